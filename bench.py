@@ -1,0 +1,303 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident batch CityHash64 on 64-byte keys (BASELINE.json).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|place]
+
+One step = one pass of the hot path (one kernel launch) over this GPU's batch
+of synthetic keys already resident in HBM.  Default workload = BASELINE
+configs[1] ("cfg2": 16M x 64 B keys per GPU, CityHash64).  For N > 1 (launched
+by torch.distributed.run) each rank hashes its own contiguous shard of the
+same key stream (keys [r*n, (r+1)*n)): independent slices, no collective on
+the data path (weak scaling); the only collectives are the timing barrier and
+the max-over-ranks of the elapsed time.
+
+Rank 0 prints one JSON line.  Besides the contract fields it carries
+  roofline      -- achieved algorithmic HBM GB/s of the hash kernel (72 B/key:
+                   64 B key read + 8 B digest write) over its average launch
+                   duration measured with HIP events on the launch stream;
+  cpu_baseline  -- the reference city.c (oracle/_ref, or the oracle port when
+                   _ref is absent) timed on this host's cores over a bounded
+                   sample of the same keys (rank 0, N = 1 only);
+  host_resident -- the same hash with keys/digests in pinned host memory
+                   (H2D + kernel + D2H pipeline), N = 1 only;
+  parity        -- digests checked against the oracle / reference golden folds.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+M = 1 << 20
+SEED_KEYS = 0x5EED5EED5EED5EED
+SEED_LENS = 0x1E575EED1E575EED
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "Gkeys/s and achieved HBM GB/s, device-resident batch CityHash64 on 64B keys"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "place"])
+    ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
+    ap.add_argument("--variant", type=int, default=0, help="64-B kernel: 0 auto, 1 direct, 2 lds, 3 window")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    if not os.path.exists(os.path.join(ROOT, "pdht_amd", "lib", "libpdht_hip.so")):
+        import __graft_entry__
+        __graft_entry__.build()
+    import pdht_amd as P
+    if a.variant:
+        P.set_variant(a.variant)
+
+    cfg = a.config
+    # ---------------------------------------------------------- workload ---
+    if cfg in ("cfg2", "cfg4", "place"):
+        L = 64 if cfg != "place" else 8
+        n = a.keys_per_gpu or 16 * M
+        first = rank * n
+        words = P.splitmix64_fill(SEED_KEYS, first * L // 8, n * L // 8, device=dev)
+        keys = words.view(torch.uint8).view(n, L)
+        dbytes = 16 if cfg == "cfg4" else 8
+        if cfg == "cfg2":
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            step = lambda: P.city64_batch(keys, out=out)  # noqa: E731
+            bytes_per_key = 64 + 8
+            workload = "cfg2: CityHash64 over 16M x 64B keys per GPU, device-resident"
+        elif cfg == "cfg4":
+            out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+            step = lambda: P.citycrc128_batch(keys, out=out)  # noqa: E731
+            bytes_per_key = 64 + 16
+            workload = "cfg4: CityHashCrc128 over 16M x 64B keys per GPU, device-resident"
+        else:
+            hist = torch.zeros(1024, dtype=torch.int64, device=dev)
+            step = lambda: P.place_batch(keys, 1, 1024, ptindex=True, rank=True, hist=hist)  # noqa: E731
+            bytes_per_key = 8 + 8 + 4 + 4
+            workload = "place: fused pdht_hash (mbits+ptindex+rank+hist) over 16M x 8B keys per GPU"
+        total_bytes_in = n * L
+    else:  # cfg3 mixed lengths
+        n = a.keys_per_gpu or 64 * M
+        first = rank * n
+        lens = P.mixed_lengths(SEED_LENS, first, n, 16, 256, device=dev)
+        offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=offs[1:])
+        total = int(offs[-1].item())
+        del lens
+        # rank 0 hashes the canonical cfg3 byte stream (golden-checked); rank r
+        # takes a disjoint segment of the same splitmix64 stream
+        words = P.splitmix64_fill(SEED_KEYS, rank << 40, (total + 7) // 8 + 2, device=dev)
+        data = words.view(torch.uint8)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        step = lambda: P.city64_var_batch(data[:total], offs, out=out)  # noqa: E731
+        bytes_per_key = total / n + 8 + 8
+        total_bytes_in = total
+        L = None
+        workload = "cfg3: CityHash64 over 64M mixed 16..256B keys per GPU (offset-indexed)"
+    torch.cuda.synchronize()
+
+    # ------------------------------------------------------------ timing ---
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    kernel_name = P.last_kernel()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record()
+        step()
+        e.record()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    # ------------------------------------------------------------ parity ---
+    parity = check_parity(P, torch, cfg, rank, world, n, first, out, locals())
+    if world > 1:
+        ok = torch.tensor([1 if parity.startswith("ok") else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()):
+            parity = "FAILED on some rank: " + parity
+
+    # ------------------------------------------------------- report ------
+    total_keys = n * world * a.steps
+    value = total_keys / elapsed / 1e9
+    achieved = bytes_per_key * n / (kern_ms / 1e3) / 1e9
+    res = {
+        "metric": METRIC if cfg == "cfg2" else f"{cfg}: Gkeys/s and achieved HBM GB/s",
+        "value": round(value, 4),
+        "unit": "Gkeys/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: splitmix64 key bytes (seed 0x5EED5EED5EED5EED), generated on device",
+        "config": {"workload": workload, "keys_per_gpu": n, "key_bytes": L,
+                   "bytes_per_key": round(bytes_per_key, 3), "kernel": kernel_name,
+                   "parallelism": f"{world} independent shards, no collective"},
+        "hbm_GBps": round(achieved * world, 1),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
+                     "traffic": load_traffic(cfg, n), "kernel_ms": round(kern_ms, 4),
+                     "kernel_ms_max_rank": round(kern_ms_max, 4),
+                     "read_only_GBps": round(total_bytes_in / (kern_ms / 1e3) / 1e9, 1)},
+        "parity": parity,
+    }
+    if rank == 0 and world == 1 and cfg in ("cfg2", "cfg4") and not a.no_host:
+        res["host_resident"] = host_rate(P, torch, n, cfg)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and cfg in ("cfg2",):
+        res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def load_traffic(cfg, n):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass, if any."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            t = json.load(f)
+        if int(t.get("keys_per_launch", -1)) != n:
+            return None
+        return t.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def check_parity(P, torch, cfg, rank, world, n, first, out, env):
+    """Bit-exact check of this rank's digests against the oracle on a sample and,
+    where the shard matches a golden config, the full fold checksum."""
+    try:
+        from oracle import oracle as O
+    except Exception as e:  # pragma: no cover
+        return f"unchecked (oracle unavailable: {e})"
+    msgs = []
+    if cfg in ("cfg2", "cfg4", "place"):
+        L = 64 if cfg != "place" else 8
+        s = min(n, 65536)
+        k = O.fixed_keys(s, L, first_key=first)
+        got = out[:s].cpu().numpy().view(np.uint64) if cfg != "place" else None
+        if cfg == "cfg2":
+            ok = (got == O.city64_fixed(k)).all()
+        elif cfg == "cfg4":
+            ok = (got.reshape(-1, 2) == O.city128_fixed(k, crc=True)).all()
+        else:
+            mb, _, _ = P.place_batch(env["keys"][:s], 1, 1024)
+            ok = (mb.cpu().numpy().view(np.uint64) == O.pdht_hash_fixed(k, 1, 1024)[0]).all()
+        msgs.append(f"{s} keys vs oracle {'ok' if ok else 'MISMATCH'}")
+        if not ok:
+            return "FAILED: " + "; ".join(msgs)
+        gf = os.path.join(ROOT, "tests", "golden", "config_folds.json")
+        if cfg in ("cfg2", "cfg4") and first == 0 and n == 16 * M and os.path.exists(gf):
+            with open(gf) as f:
+                folds = json.load(f)["configs"]
+            key = "cfg2_city64_16M_x64" if cfg == "cfg2" else "cfg4_crc128_16M_x64"
+            d = out.reshape(-1)
+            idx = torch.arange(d.numel(), device=d.device, dtype=torch.int64)
+            fold = int((d * (2 * idx + 1)).sum().item()) & 0xFFFFFFFFFFFFFFFF
+            if f"{fold:016x}" != folds[key]["total"]:
+                return "FAILED: full fold mismatch vs reference golden " + key
+            msgs.append(f"full {n}-key fold == reference golden ({key})")
+    else:
+        offs = env["offs"][: 65537].cpu().numpy().astype(np.uint64)
+        data = env["data"][: int(offs[-1])].cpu().numpy()
+        ok = (out[:65536].cpu().numpy().view(np.uint64) == O.city64_var(data, offs)).all()
+        msgs.append(f"65536 mixed keys vs oracle {'ok' if ok else 'MISMATCH'}")
+        if not ok:
+            return "FAILED: " + "; ".join(msgs)
+    return "ok: " + "; ".join(msgs)
+
+
+def host_rate(P, torch, n, cfg):
+    """Host-resident rate: pinned keys in, pinned digests out, through the
+    C-ABI's chunked multi-stream pipeline (PCIe-bound)."""
+    try:
+        m = min(n, 16 * M)
+        keys = torch.empty((m, 64), dtype=torch.uint8).pin_memory()
+        keys.view(-1).view(torch.int64).copy_(P.splitmix64_fill(SEED_KEYS, 0, m * 8).cpu())
+        w = 2 if cfg == "cfg4" else 1
+        out = torch.empty((m, w) if w == 2 else (m,), dtype=torch.int64).pin_memory()
+        fn = P.citycrc128_batch_host if cfg == "cfg4" else P.city64_batch_host
+        fn(keys, out=out)  # warm-up (allocates the pipeline buffers)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn(keys, out=out)
+        dt = (time.perf_counter() - t0) / reps
+        return {"value": round(m / dt / 1e9, 4), "unit": "Gkeys/s", "keys": m,
+                "GBps_pcie": round(m * (64 + 8 * w) / dt / 1e9, 2),
+                "note": "pinned host keys -> H2D -> kernel -> D2H -> pinned host digests"}
+    except Exception as e:  # pragma: no cover
+        return {"error": str(e)}
+
+
+def cpu_baseline(budget_s: float):
+    """Reference city.c (oracle/_ref) on this host's cores over a bounded
+    sample: 4M x 64B keys of the same stream, repeated to fill ~budget_s."""
+    from oracle import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    s = 4 * M
+    keys = O.fixed_keys(s, 64)
+    secs, out, kind = O.time_city64(keys, threads, 1)
+    reps = max(1, int(budget_s / max(secs, 1e-6)))
+    secs, out, kind = O.time_city64(keys, threads, reps)
+    ok = bool((out[:4096] == O.city64_fixed(keys[:4096])).all())
+    one, _, _ = O.time_city64(keys[: M // 2], 1, 1)
+    return {"value": round(s * reps / secs / 1e9, 4), "unit": "Gkeys/s", "cores": threads,
+            "kind": kind, "sample": f"{reps} passes over 4M x 64B keys ({threads} pthreads, "
+                                    f"{secs:.2f} s wall, {secs * threads:.1f} CPU-s)",
+            "single_thread_Gkeys_s": round((M // 2) / one / 1e9, 4), "digests_ok": ok}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * pdht_hip.h -- C-ABI of the MI355X batch key-hashing engine.
+ *
+ * The reference hashes one key per call on the initiator CPU
+ * (dht->hashfn -> pdht_hash -> CityHash64, libpdht/putget.c:53,
+ * libpdht/hash.c:25-30).  This header adds the batch entry points a caller
+ * (a bulk loader such as bench/Meraculous/buildUFXhashBinary.h:83-112, or
+ * pdht_hash_batch in pdht_hash.h) binds to hash many keys at once on a GPU.
+ * Plain pointers and sizes only: no HIP or torch types appear, a stream is an
+ * opaque pointer (a hipStream_t may be passed; NULL = the default stream).
+ *
+ * Every function returns 0 (== PdhtStatusOK, libpdht/pdht.h:178-184) on
+ * success and PDHT_HIP_ERROR (== PdhtStatusError) otherwise; the reason is
+ * kept per thread in pdht_hip_last_error().  Nothing here falls back to the
+ * CPU: with no usable GPU the batch calls fail.
+ *
+ * Digest layouts: 64-bit digests are one uint64 per key; 128-bit digests are
+ * two uint64 per key, {first (low), second (high)} exactly as the
+ * reference's uint128 (city.h:58-65).
+ *
+ * Key layouts:
+ *   fixed  -- key i occupies bytes [i*stride, i*stride + keylen) of `keys`
+ *             (stride >= keylen; stride == keylen for packed keys);
+ *   var    -- key i occupies bytes [offsets[i], offsets[i+1]) of `bytes`;
+ *             offsets has n+1 non-decreasing entries.
+ */
+#ifndef PDHT_HIP_H_
+#define PDHT_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDHT_HIP_OK 0
+#define PDHT_HIP_ERROR 1 /* == PdhtStatusError */
+
+typedef struct ihipStream_t *pdht_hip_stream_t; /* layout of hipStream_t */
+
+/* ---- runtime ------------------------------------------------------------ */
+const char *pdht_hip_version(void);
+/* Last error message of the calling thread ("" if none). */
+const char *pdht_hip_last_error(void);
+/* Number of visible GPUs (0 on a host without one; still returns OK). */
+int pdht_hip_device_count(int *count);
+/* Make `device` current for the calling thread (hipSetDevice) and
+ * initialise its per-device state once. */
+int pdht_hip_set_device(int device);
+
+/* ---- device-resident batches (all pointers are device pointers) --------- */
+/* CityHash64 (city.h:68) over fixed-length keys. */
+int pdht_city64_batch_dev(const void *keys, size_t stride, size_t keylen,
+                          size_t n, uint64_t *out, pdht_hip_stream_t stream);
+/* CityHash64WithSeeds (city.h:76); CityHash64WithSeed(s) == seeds(k2, s). */
+int pdht_city64_seeds_batch_dev(const void *keys, size_t stride, size_t keylen,
+                                size_t n, uint64_t seed0, uint64_t seed1,
+                                uint64_t *out, pdht_hip_stream_t stream);
+/* CityHash64 over variable-length keys. */
+int pdht_city64_batch_var_dev(const void *bytes, const uint64_t *offsets,
+                              size_t n, uint64_t *out,
+                              pdht_hip_stream_t stream);
+/* CityHash128 (city.h:80): out[2i] = first, out[2i+1] = second. */
+int pdht_city128_batch_dev(const void *keys, size_t stride, size_t keylen,
+                           size_t n, uint64_t *out, pdht_hip_stream_t stream);
+/* CityHash128WithSeed (city.h:84). */
+int pdht_city128_seed_batch_dev(const void *keys, size_t stride, size_t keylen,
+                                size_t n, uint64_t seed_lo, uint64_t seed_hi,
+                                uint64_t *out, pdht_hip_stream_t stream);
+int pdht_city128_batch_var_dev(const void *bytes, const uint64_t *offsets,
+                               size_t n, uint64_t *out,
+                               pdht_hip_stream_t stream);
+/* CityHashCrc128 (citycrc.h:39). */
+int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen,
+                              size_t n, uint64_t *out,
+                              pdht_hip_stream_t stream);
+/* CityHashCrc128WithSeed (citycrc.h:43). */
+int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride,
+                                   size_t keylen, size_t n, uint64_t seed_lo,
+                                   uint64_t seed_hi, uint64_t *out,
+                                   pdht_hip_stream_t stream);
+int pdht_citycrc128_batch_var_dev(const void *bytes, const uint64_t *offsets,
+                                  size_t n, uint64_t *out,
+                                  pdht_hip_stream_t stream);
+
+/* Fused placement = pdht_hash (libpdht/hash.c:25-30) over a batch of packed
+ * keysize-byte keys:
+ *   mbits[i]   = CityHash64(key_i, keysize)
+ *   ptindex[i] = mbits[i] % nptes                 (skipped if ptindex NULL)
+ *   rank_i     = mbits[i] % nranks, stored as a uint32 at
+ *                (char*)rank + i*rank_stride       (skipped if rank NULL;
+ *                rank_stride 8 writes the .rank member of a ptl_process_t
+ *                array, 4 a dense uint32 array)
+ *   hist[r]   += number of keys placed on rank r  (skipped if hist NULL;
+ *                nranks uint64 counters, accumulated, not cleared) -- the
+ *                rankputs[] statistic of putget.c:55 / util.c:386-397. */
+int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
+                         uint32_t nptes, uint32_t nranks, uint64_t *mbits,
+                         uint32_t *ptindex, void *rank, size_t rank_stride,
+                         uint64_t *hist, pdht_hip_stream_t stream);
+
+/* ---- host-resident batches ---------------------------------------------- */
+/* Keys and digests in host memory.  Chunks are copied H2D, hashed and copied
+ * back D2H on several streams so copies and kernels overlap; pinned
+ * (hipHostMalloc / registered) buffers are DMA'd directly, pageable ones go
+ * through pinned staging.  Blocking: returns when `out` is complete. */
+int pdht_city64_batch_host(const void *keys, size_t keylen, size_t n,
+                           uint64_t *out, int device);
+int pdht_city64_batch_var_host(const void *bytes, const uint64_t *offsets,
+                               size_t n, uint64_t *out, int device);
+int pdht_citycrc128_batch_host(const void *keys, size_t keylen, size_t n,
+                               uint64_t *out, int device);
+int pdht_place_batch_host(const void *keys, size_t keysize, size_t n,
+                          uint32_t nptes, uint32_t nranks, uint64_t *mbits,
+                          uint32_t *ptindex, void *rank, size_t rank_stride,
+                          int device);
+
+/* ---- synthetic workloads (benchmarks/tests) ----------------------------- */
+/* out[w] = splitmix64 output number (first + w) of the stream seeded `seed`:
+ * z = seed + (first+w+1)*0x9e3779b97f4a7c15, then the splitmix64 finaliser. */
+int pdht_hip_splitmix64_fill_dev(uint64_t seed, uint64_t first, size_t nwords,
+                                 uint64_t *out, pdht_hip_stream_t stream);
+/* lens[i] = lo + splitmix64(seed)[first+i] % (hi - lo + 1) */
+int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
+                               uint32_t lo, uint32_t hi, uint64_t *lens,
+                               pdht_hip_stream_t stream);
+
+/* ---- engine tuning / introspection -------------------------------------- */
+/* Kernel variant used by pdht_city64_batch_dev for 64-byte packed keys:
+ * 0 = auto, 1 = direct (per-lane 16-B loads), 2 = LDS-transposed,
+ * 3 = generic LDS window.  Returns the previous value. */
+int pdht_hip_set_variant(int variant);
+/* Name of the kernel the last batch call on this thread launched. */
+const char *pdht_hip_last_kernel(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDHT_HIP_H_ */

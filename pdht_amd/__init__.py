@@ -1,0 +1,497 @@
+"""pdht_amd -- MI355X batch key-hashing engine for pdht's CityHash path.
+
+Python view of the C-ABI in include/pdht_hip.h / pdht_city.h / pdht_hash.h,
+loaded from the in-tree pdht_amd/lib/libpdht_hip.so (built by `make` or
+__graft_entry__.build()).  There is no fallback: if the library is missing
+the import fails, and the batch entry points fail when no GPU is usable.
+
+torch is used only as device-memory / stream plumbing: tensors are passed to
+the C-ABI as raw pointers on torch's current HIP stream.
+
+Mirrors of the reference interface:
+  CityHash64 / CityHash64WithSeed(s) / CityHash128(WithSeed) /
+  CityHashCrc128(WithSeed) / CityHashCrc256   -- city.h:68-84, citycrc.h:39-46
+  PdhtTable.hash (pdht_hash, hash.c:25-30), PdhtTable.sethash (hash.c:39-41)
+Batch API (new): city64_batch, city128_batch, citycrc128_batch, *_var,
+place_batch (fused pdht_hash over a batch), *_host variants.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libpdht_hip.so")
+
+__all__ = [
+    "lib", "LIB_PATH", "PdhtError", "CityHash64", "CityHash64WithSeed", "CityHash64WithSeeds",
+    "CityHash128", "CityHash128WithSeed", "CityHashCrc128", "CityHashCrc128WithSeed",
+    "CityHashCrc256", "city64_batch", "city64_seeds_batch", "city64_var_batch", "city128_batch",
+    "city128_seed_batch", "city128_var_batch", "citycrc128_batch", "citycrc128_seed_batch",
+    "citycrc128_var_batch", "place_batch", "city64_batch_host", "city64_var_batch_host",
+    "citycrc128_batch_host", "place_batch_host", "splitmix64_fill", "mixed_lengths",
+    "device_count", "PdhtTable", "K2",
+]
+
+K2 = 0x9AE16A3B2F90404F  # city.c:96 (CityHash64WithSeed's seed0)
+
+
+class PdhtError(RuntimeError):
+    pass
+
+
+class Uint128(C.Structure):
+    """city.h:58-65"""
+
+    _fields_ = [("first", C.c_uint64), ("second", C.c_uint64)]
+
+
+class PtlProcess(C.Union):
+    """ptl_process_t stand-in (portals4.h): 8 bytes, .rank is the low uint32."""
+
+    class _Phys(C.Structure):
+        _fields_ = [("nid", C.c_uint32), ("pid", C.c_uint32)]
+
+    _fields_ = [("phys", _Phys), ("rank", C.c_uint32)]
+
+
+_HASHFUNC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64),
+                        C.POINTER(C.c_uint32), C.POINTER(PtlProcess))
+
+
+class _PdhtT(C.Structure):
+    """Stand-in pdht_t of include/pdht_hash.h (keysize, hashfn, ptl.nptes)."""
+
+    _fields_ = [("keysize", C.c_uint), ("hashfn", C.c_void_p), ("nptes", C.c_uint)]
+
+
+_lib = None
+_V = C.c_void_p
+_S = C.c_size_t
+_U64 = C.c_uint64
+_U32 = C.c_uint32
+
+
+def _declare(L):
+    sig = {
+        "pdht_hip_version": (C.c_char_p, []),
+        "pdht_hip_last_error": (C.c_char_p, []),
+        "pdht_hip_last_kernel": (C.c_char_p, []),
+        "pdht_hip_set_variant": (C.c_int, [C.c_int]),
+        "pdht_hip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "pdht_hip_set_device": (C.c_int, [C.c_int]),
+        "pdht_city64_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
+        "pdht_city64_seeds_batch_dev": (C.c_int, [_V, _S, _S, _S, _U64, _U64, _V, _V]),
+        "pdht_city64_batch_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_city128_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
+        "pdht_city128_seed_batch_dev": (C.c_int, [_V, _S, _S, _S, _U64, _U64, _V, _V]),
+        "pdht_city128_batch_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_citycrc128_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
+        "pdht_citycrc128_seed_batch_dev": (C.c_int, [_V, _S, _S, _S, _U64, _U64, _V, _V]),
+        "pdht_citycrc128_batch_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_place_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _V, _V, _S, _V, _V]),
+        "pdht_city64_batch_host": (C.c_int, [_V, _S, _S, _V, C.c_int]),
+        "pdht_city64_batch_var_host": (C.c_int, [_V, _V, _S, _V, C.c_int]),
+        "pdht_citycrc128_batch_host": (C.c_int, [_V, _S, _S, _V, C.c_int]),
+        "pdht_place_batch_host": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _V, _V, _S, C.c_int]),
+        "pdht_hip_splitmix64_fill_dev": (C.c_int, [_U64, _U64, _S, _V, _V]),
+        "pdht_hip_mixed_lengths_dev": (C.c_int, [_U64, _U64, _S, _U32, _U32, _V, _V]),
+        "CityHash64": (_U64, [_V, _S]),
+        "CityHash64WithSeed": (_U64, [_V, _S, _U64]),
+        "CityHash64WithSeeds": (_U64, [_V, _S, _U64, _U64]),
+        "CityHash128": (Uint128, [_V, _S]),
+        "CityHash128WithSeed": (Uint128, [_V, _S, Uint128]),
+        "CityHashCrc128": (Uint128, [_V, _S]),
+        "CityHashCrc128WithSeed": (Uint128, [_V, _S, Uint128]),
+        "CityHashCrc256": (None, [_V, _S, C.POINTER(C.c_uint64)]),
+        "pdht_hash": (None, [_V, _V, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                             C.POINTER(PtlProcess)]),
+        "pdht_sethash": (None, [_V, _V]),
+        "pdht_hash_batch": (C.c_int, [_V, _V, _S, _V, _V, _V, C.c_int]),
+        "pdht_hash_batch_dev": (C.c_int, [_V, _V, _S, _V, _V, _V, _V, _V]),
+        "pdht_hip_table_init": (None, [_V, C.c_uint, C.c_uint]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def lib():
+    """The product library (loaded once).  Raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C {ROOT}` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise PdhtError(f"{what}: {lib().pdht_hip_last_error().decode()}")
+
+
+def last_kernel() -> str:
+    return lib().pdht_hip_last_kernel().decode()
+
+
+def set_variant(v: int) -> int:
+    return lib().pdht_hip_set_variant(v)
+
+
+def device_count() -> int:
+    c = C.c_int(0)
+    _check(lib().pdht_hip_device_count(C.byref(c)), "device_count")
+    return c.value
+
+
+# ------------------------------------------------------------ scalar API ---
+def _cbuf(data):
+    if isinstance(data, np.ndarray):
+        return C.c_void_p(data.ctypes.data), data.nbytes
+    b = bytes(data)
+    return C.c_char_p(b), len(b)
+
+
+def CityHash64(data) -> int:
+    p, n = _cbuf(data)
+    return lib().CityHash64(p, n)
+
+
+def CityHash64WithSeed(data, seed: int) -> int:
+    p, n = _cbuf(data)
+    return lib().CityHash64WithSeed(p, n, seed)
+
+
+def CityHash64WithSeeds(data, seed0: int, seed1: int) -> int:
+    p, n = _cbuf(data)
+    return lib().CityHash64WithSeeds(p, n, seed0, seed1)
+
+
+def CityHash128(data) -> tuple[int, int]:
+    p, n = _cbuf(data)
+    r = lib().CityHash128(p, n)
+    return r.first, r.second
+
+
+def CityHash128WithSeed(data, seed: tuple[int, int]) -> tuple[int, int]:
+    p, n = _cbuf(data)
+    r = lib().CityHash128WithSeed(p, n, Uint128(*seed))
+    return r.first, r.second
+
+
+def CityHashCrc128(data) -> tuple[int, int]:
+    p, n = _cbuf(data)
+    r = lib().CityHashCrc128(p, n)
+    return r.first, r.second
+
+
+def CityHashCrc128WithSeed(data, seed: tuple[int, int]) -> tuple[int, int]:
+    p, n = _cbuf(data)
+    r = lib().CityHashCrc128WithSeed(p, n, Uint128(*seed))
+    return r.first, r.second
+
+
+def CityHashCrc256(data) -> tuple[int, int, int, int]:
+    p, n = _cbuf(data)
+    out = (C.c_uint64 * 4)()
+    lib().CityHashCrc256(p, n, out)
+    return tuple(out)
+
+
+# ----------------------------------------------------- device batch API ---
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_ptr(stream=None):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _dptr(t) -> C.c_void_p:
+    return C.c_void_p(t.data_ptr())
+
+
+def _keys_2d(keys):
+    """keys: uint8 CUDA tensor [n, L] with unit inner stride (rows may be strided)."""
+    torch = _torch()
+    if keys.dtype != torch.uint8 or keys.dim() != 2 or not keys.is_cuda:
+        raise ValueError("keys must be a CUDA uint8 tensor of shape [n, keylen]")
+    if keys.stride(1) != 1:
+        raise ValueError("keys rows must be contiguous")
+    n, L = keys.shape
+    stride = keys.stride(0) if n > 1 else L
+    return n, L, stride
+
+
+def _out(n, words, device, out=None):
+    torch = _torch()
+    shape = (n,) if words == 1 else (n, words)
+    if out is None:
+        return torch.empty(shape, dtype=torch.int64, device=device)
+    if out.dtype != torch.int64 or tuple(out.shape) != shape or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous int64 tensor of shape {shape}")
+    return out
+
+
+def city64_batch(keys, out=None, stream=None):
+    """CityHash64 of each row of keys [n, L] (uint8, CUDA) -> int64 [n] (bit pattern of u64)."""
+    n, L, stride = _keys_2d(keys)
+    out = _out(n, 1, keys.device, out)
+    _check(lib().pdht_city64_batch_dev(_dptr(keys), stride, L, n, _dptr(out), _stream_ptr(stream)),
+           "pdht_city64_batch_dev")
+    return out
+
+
+def city64_seeds_batch(keys, seed0: int, seed1: int, out=None, stream=None):
+    n, L, stride = _keys_2d(keys)
+    out = _out(n, 1, keys.device, out)
+    _check(lib().pdht_city64_seeds_batch_dev(_dptr(keys), stride, L, n, seed0, seed1, _dptr(out),
+                                             _stream_ptr(stream)), "pdht_city64_seeds_batch_dev")
+    return out
+
+
+def city64_seed_batch(keys, seed: int, out=None, stream=None):
+    """CityHash64WithSeed == WithSeeds(k2, seed) (city.c:265-267)."""
+    return city64_seeds_batch(keys, K2, seed, out, stream)
+
+
+def _check_var(data, offsets):
+    torch = _torch()
+    if data.dtype != torch.uint8 or not data.is_cuda or not data.is_contiguous():
+        raise ValueError("data must be a contiguous CUDA uint8 tensor")
+    if offsets.dtype != torch.int64 or not offsets.is_cuda or not offsets.is_contiguous():
+        raise ValueError("offsets must be a contiguous CUDA int64 tensor of n+1 entries")
+    return offsets.numel() - 1
+
+
+def city64_var_batch(data, offsets, out=None, stream=None):
+    n = _check_var(data, offsets)
+    out = _out(n, 1, data.device, out)
+    _check(lib().pdht_city64_batch_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
+                                           _stream_ptr(stream)), "pdht_city64_batch_var_dev")
+    return out
+
+
+def city128_batch(keys, out=None, stream=None):
+    n, L, stride = _keys_2d(keys)
+    out = _out(n, 2, keys.device, out)
+    _check(lib().pdht_city128_batch_dev(_dptr(keys), stride, L, n, _dptr(out), _stream_ptr(stream)),
+           "pdht_city128_batch_dev")
+    return out
+
+
+def city128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
+    n, L, stride = _keys_2d(keys)
+    out = _out(n, 2, keys.device, out)
+    _check(lib().pdht_city128_seed_batch_dev(_dptr(keys), stride, L, n, seed[0], seed[1], _dptr(out),
+                                             _stream_ptr(stream)), "pdht_city128_seed_batch_dev")
+    return out
+
+
+def city128_var_batch(data, offsets, out=None, stream=None):
+    n = _check_var(data, offsets)
+    out = _out(n, 2, data.device, out)
+    _check(lib().pdht_city128_batch_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
+                                            _stream_ptr(stream)), "pdht_city128_batch_var_dev")
+    return out
+
+
+def citycrc128_batch(keys, out=None, stream=None):
+    n, L, stride = _keys_2d(keys)
+    out = _out(n, 2, keys.device, out)
+    _check(lib().pdht_citycrc128_batch_dev(_dptr(keys), stride, L, n, _dptr(out),
+                                           _stream_ptr(stream)), "pdht_citycrc128_batch_dev")
+    return out
+
+
+def citycrc128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
+    n, L, stride = _keys_2d(keys)
+    out = _out(n, 2, keys.device, out)
+    _check(lib().pdht_citycrc128_seed_batch_dev(_dptr(keys), stride, L, n, seed[0], seed[1],
+                                                _dptr(out), _stream_ptr(stream)),
+           "pdht_citycrc128_seed_batch_dev")
+    return out
+
+
+def citycrc128_var_batch(data, offsets, out=None, stream=None):
+    n = _check_var(data, offsets)
+    out = _out(n, 2, data.device, out)
+    _check(lib().pdht_citycrc128_batch_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
+                                               _stream_ptr(stream)), "pdht_citycrc128_batch_var_dev")
+    return out
+
+
+def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=None,
+                stream=None):
+    """Fused pdht_hash (hash.c:25-30) over keys [n, keysize] (packed, CUDA).
+
+    Returns (mbits int64[n], ptindex int32[n] | None, rank int32[n] | None);
+    if `hist` (int64[nranks], CUDA) is given, per-rank counts are added to it.
+    """
+    torch = _torch()
+    n, L, stride = _keys_2d(keys)
+    if stride != L:
+        raise ValueError("place_batch needs packed keys")
+    mb = torch.empty(n, dtype=torch.int64, device=keys.device)
+    pt = torch.empty(n, dtype=torch.int32, device=keys.device) if ptindex else None
+    rk = torch.empty(n, dtype=torch.int32, device=keys.device) if rank else None
+    _check(lib().pdht_place_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(mb),
+                                      _dptr(pt) if pt is not None else None,
+                                      _dptr(rk) if rk is not None else None, 4,
+                                      _dptr(hist) if hist is not None else None,
+                                      _stream_ptr(stream)), "pdht_place_batch_dev")
+    return mb, pt, rk
+
+
+def splitmix64_fill(seed: int, first: int, nwords: int, out=None, device="cuda", stream=None):
+    torch = _torch()
+    if out is None:
+        out = torch.empty(nwords, dtype=torch.int64, device=device)
+    _check(lib().pdht_hip_splitmix64_fill_dev(seed, first, nwords, _dptr(out), _stream_ptr(stream)),
+           "pdht_hip_splitmix64_fill_dev")
+    return out
+
+
+def mixed_lengths(seed: int, first: int, n: int, lo: int, hi: int, device="cuda", stream=None):
+    torch = _torch()
+    out = torch.empty(n, dtype=torch.int64, device=device)
+    _check(lib().pdht_hip_mixed_lengths_dev(seed, first, n, lo, hi, _dptr(out), _stream_ptr(stream)),
+           "pdht_hip_mixed_lengths_dev")
+    return out
+
+
+# ------------------------------------------------------- host batch API ---
+def _np_keys(keys: np.ndarray):
+    if keys.dtype != np.uint8 or keys.ndim != 2 or not keys.flags["C_CONTIGUOUS"]:
+        raise ValueError("keys must be a C-contiguous uint8 array [n, keylen]")
+    return keys.shape
+
+
+def _host_ptr(a):
+    """numpy array or (pinned) CPU torch tensor -> address."""
+    if isinstance(a, np.ndarray):
+        return C.c_void_p(a.ctypes.data)
+    return C.c_void_p(a.data_ptr())
+
+
+def city64_batch_host(keys, out=None, device: int = 0):
+    """Host-resident keys (numpy uint8 [n, L] or pinned CPU tensor) -> uint64 [n]."""
+    n, L = keys.shape
+    if out is None:
+        out = np.empty(n, dtype=np.uint64)
+    _check(lib().pdht_city64_batch_host(_host_ptr(keys), L, n, _host_ptr(out), device),
+           "pdht_city64_batch_host")
+    return out
+
+
+def city64_var_batch_host(data: np.ndarray, offsets: np.ndarray, out=None, device: int = 0):
+    n = offsets.size - 1
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if out is None:
+        out = np.empty(n, dtype=np.uint64)
+    _check(lib().pdht_city64_batch_var_host(_host_ptr(data), _host_ptr(offsets), n, _host_ptr(out),
+                                            device), "pdht_city64_batch_var_host")
+    return out
+
+
+def citycrc128_batch_host(keys, out=None, device: int = 0):
+    n, L = keys.shape
+    if out is None:
+        out = np.empty((n, 2), dtype=np.uint64)
+    _check(lib().pdht_citycrc128_batch_host(_host_ptr(keys), L, n, _host_ptr(out), device),
+           "pdht_citycrc128_batch_host")
+    return out
+
+
+def place_batch_host(keys: np.ndarray, nptes: int, nranks: int, device: int = 0):
+    n, L = _np_keys(keys)
+    mb = np.empty(n, dtype=np.uint64)
+    pt = np.empty(n, dtype=np.uint32)
+    rk = np.empty(n, dtype=np.uint32)
+    _check(lib().pdht_place_batch_host(_host_ptr(keys), L, n, nptes, nranks, _host_ptr(mb),
+                                       _host_ptr(pt), _host_ptr(rk), 4, device),
+           "pdht_place_batch_host")
+    return mb, pt, rk
+
+
+# ------------------------------------------------------- pdht_t mirror ---
+class PdhtTable:
+    """The hash-path view of a pdht table (pdht_create's keysize/nptes,
+    init.c:80-94) over the stand-in pdht_t of include/pdht_hash.h.
+
+    hash(key)            -> (mbits, ptindex, rank)       pdht_hash, hash.c:25-30
+    sethash(fn)          -> install a plugin              pdht_sethash, hash.c:39-41
+    hash_batch(keys)     -> arrays                        pdht_hash_batch (GPU or plugin)
+    """
+
+    def __init__(self, keysize: int, nptes: int = 1, nranks: int = 1):
+        self._t = _PdhtT()
+        lib().pdht_hip_table_init(C.byref(self._t), keysize, nptes)
+        self.nranks = nranks
+        self._plugin = None
+
+    @property
+    def keysize(self) -> int:
+        return self._t.keysize
+
+    @property
+    def nptes(self) -> int:
+        return self._t.nptes
+
+    def _set_ranks(self):
+        C.c_int.in_dll(lib(), "pdht_hip_shim_nranks").value = self.nranks
+
+    def sethash(self, fn):
+        """fn(table, key_bytes) -> (mbits, ptindex, rank) or a raw C function pointer."""
+        if fn is None:
+            lib().pdht_sethash(C.byref(self._t), C.cast(lib().pdht_hash, C.c_void_p))
+            self._plugin = None
+            return
+        L = self.keysize
+
+        def tramp(dht, key, mb, pt, rk):
+            m, p, r = fn(self, C.string_at(key, L))
+            mb[0] = m & 0xFFFFFFFFFFFFFFFF
+            pt[0] = p & 0xFFFFFFFF
+            rk[0].rank = r & 0xFFFFFFFF
+
+        self._plugin = _HASHFUNC(tramp)
+        lib().pdht_sethash(C.byref(self._t), C.cast(self._plugin, C.c_void_p))
+
+    def hash(self, key: bytes):
+        if len(key) < self.keysize:
+            raise ValueError("key shorter than keysize")
+        self._set_ranks()
+        mb, pt, rk = C.c_uint64(), C.c_uint32(), PtlProcess()
+        # dht->hashfn(dht, key, &mbits, &ptindex, &rank), as putget.c:53 calls it
+        fn = _HASHFUNC(self._t.hashfn)
+        fn(C.cast(C.byref(self._t), C.c_void_p), C.c_char_p(bytes(key)), C.byref(mb), C.byref(pt),
+           C.byref(rk))
+        return mb.value, pt.value, rk.rank
+
+    def hash_batch(self, keys: np.ndarray, device: int = 0):
+        """keys uint8 [n, keysize] (host) -> (mbits u64[n], ptindex u32[n], rank u32[n])."""
+        n, L = _np_keys(keys)
+        if L != self.keysize:
+            raise ValueError("key width != keysize")
+        self._set_ranks()
+        mb = np.empty(n, dtype=np.uint64)
+        pt = np.empty(n, dtype=np.uint32)
+        rk = (PtlProcess * max(n, 1))()
+        _check(lib().pdht_hash_batch(C.byref(self._t), _host_ptr(keys), n, _host_ptr(mb),
+                                     _host_ptr(pt), C.cast(rk, C.c_void_p), device),
+               "pdht_hash_batch")
+        ranks = np.frombuffer(rk, dtype=np.uint32).reshape(-1, 2)[:n, 0].copy()
+        return mb, pt, ranks

@@ -1,0 +1,448 @@
+// city_core.h -- CityHash v1.0.x arithmetic, written once for host and gfx950.
+//
+// Product code (not the oracle).  Every function is __host__ __device__ and
+// templated on a *reader*: the object that supplies little-endian words of
+// the key at byte offsets.  The same algorithm body is therefore compiled for
+//   * the scalar host API (HostReader: plain memory)          -> city_host.cpp
+//   * fixed-length keys held in VGPRs (RegReader<L>)           -> kernels
+//   * keys staged in LDS at arbitrary byte offsets (LdsReader) -> kernels
+//   * keys read straight from global memory (GlobalReader)     -> kernels
+// With a compile-time length (RegReader<L>) the length dispatch, every byte
+// offset and every rotate amount fold to constants, so the 64-byte path is
+// straight-line VALU over 16 registers.
+//
+// Behaviour follows /root/reference/libpdht/city.c; each routine cites the
+// lines whose semantics it reproduces.  Parity: tests/ (oracle + golden).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#define PDHT_HD __host__ __device__ __forceinline__
+
+namespace pdht {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+struct u128 {  // city.h:58-65: first = low 64 bits, second = high 64 bits
+  u64 lo, hi;
+};
+
+// city.c:94-97, :103
+constexpr u64 kK0 = 0xc3a5c85c97cb3127ULL;
+constexpr u64 kK1 = 0xb492b66fbe98f273ULL;
+constexpr u64 kK2 = 0x9ae16a3b2f90404fULL;
+constexpr u64 kK3 = 0xc949d7c7509e6557ULL;
+constexpr u64 kMul = 0x9ddfea08eb382d69ULL;
+
+// ---------------------------------------------------------------- bit ops ---
+// city.c:115-125.  `s` is 1..63 at every call site except the runtime rotate
+// of HashLen0to16 (9..16) -- both covered by rotr_nz; rotr keeps the shift-0
+// guard of Rotate() for the generic callers.
+PDHT_HD u64 rotr_nz(u64 v, u32 s) { return (v >> s) | (v << (64 - s)); }
+PDHT_HD u64 rotr(u64 v, u32 s) { return s == 0 ? v : rotr_nz(v, s); }
+PDHT_HD u64 smix(u64 v) { return v ^ (v >> 47); }  // city.c:127-129
+
+// city.c:101-110 Hash128to64 == city.c:131-136 HashLen16(u, v)
+PDHT_HD u64 mix16(u64 u, u64 v) {
+  u64 a = smix((u ^ v) * kMul);
+  u64 b = smix((v ^ a) * kMul);
+  return b * kMul;
+}
+
+// ---------------------------------------------------------------- readers ---
+// A reader R exposes: u64 w64(u32 off), u32 w32(u32 off), u32 b8(u32 off)
+// and R at(u32 off) (a reader re-based `off` bytes further).
+
+struct HostReader {
+  const uint8_t *p;
+  PDHT_HD u64 w64(size_t o) const {
+    u64 r;
+    memcpy(&r, p + o, 8);
+    return r;
+  }
+  PDHT_HD u32 w32(size_t o) const {
+    u32 r;
+    memcpy(&r, p + o, 4);
+    return r;
+  }
+  PDHT_HD u32 b8(size_t o) const { return p[o]; }
+  PDHT_HD HostReader at(size_t o) const { return HostReader{p + o}; }
+};
+
+// Key bytes held in registers as W little-endian dwords; offsets are expected
+// to be compile-time constants after inlining (fixed-length kernels).
+template <int W>
+struct RegReader {
+  u32 d[W];
+  u32 base;  // byte offset of this view inside d (compile-time constant)
+  PDHT_HD u32 dw(u32 byte_off) const {  // dword at any byte offset
+    const u32 q = byte_off >> 2, r = byte_off & 3;
+    if (r == 0) return d[q];
+    const u32 hi = (q + 1 < (u32)W) ? d[q + 1] : 0u;
+    return (u32)((((u64)hi << 32) | d[q]) >> (8 * r));
+  }
+  PDHT_HD u64 w64(u32 o) const {
+    o += base;
+    return ((u64)dw(o + 4) << 32) | dw(o);
+  }
+  PDHT_HD u32 w32(u32 o) const { return dw(o + base); }
+  PDHT_HD u32 b8(u32 o) const { return (dw(o + base)) & 0xffu; }
+  PDHT_HD RegReader at(u32 o) const {
+    RegReader r = *this;
+    r.base += o;
+    return r;
+  }
+};
+
+// ----------------------------------------------------------- CityHash64 ---
+// city.c:138-157
+template <class R>
+PDHT_HD u64 len0to16(const R &s, u64 len) {
+  if (len > 8) {
+    const u64 a = s.w64(0);
+    const u64 b = s.w64((u32)len - 8);
+    return mix16(a, rotr_nz(b + len, (u32)len)) ^ b;
+  }
+  if (len >= 4) {
+    const u64 a = s.w32(0);
+    return mix16(len + (a << 3), (u64)s.w32((u32)len - 4));
+  }
+  if (len > 0) {
+    const u32 a = s.b8(0), b = s.b8((u32)len >> 1), c = s.b8((u32)len - 1);
+    const u32 y = a + (b << 8);
+    const u32 z = (u32)len + (c << 2);
+    return smix((u64)y * kK2 ^ (u64)z * kK3) * kK2;
+  }
+  return kK2;
+}
+
+// city.c:161-168
+template <class R>
+PDHT_HD u64 len17to32(const R &s, u64 len) {
+  const u32 n = (u32)len;
+  const u64 a = s.w64(0) * kK1;
+  const u64 b = s.w64(8);
+  const u64 c = s.w64(n - 8) * kK2;
+  const u64 d = s.w64(n - 16) * kK0;
+  return mix16(rotr_nz(a - b, 43) + rotr_nz(c, 30) + d,
+               a + rotr_nz(b ^ kK3, 20) - c + len);
+}
+
+// city.c:173-198 -- WeakHashLen32WithSeeds over four given words
+PDHT_HD u128 weak32(u64 w, u64 x, u64 y, u64 z, u64 a, u64 b) {
+  a += w;
+  b = rotr_nz(b + a + z, 21);
+  const u64 c = a;
+  a += x;
+  a += y;
+  b += rotr_nz(a, 44);
+  return u128{a + z, b + c};
+}
+template <class R>
+PDHT_HD u128 weak32_at(const R &s, u32 o, u64 a, u64 b) {
+  return weak32(s.w64(o), s.w64(o + 8), s.w64(o + 16), s.w64(o + 24), a, b);
+}
+
+// city.c:201-222 -- the 33..64-byte path (the 64-byte key hot path)
+template <class R>
+PDHT_HD u64 len33to64(const R &s, u64 len) {
+  const u32 n = (u32)len;
+  u64 z = s.w64(24);
+  u64 a = s.w64(0) + (len + s.w64(n - 16)) * kK0;
+  u64 b = rotr_nz(a + z, 52);
+  u64 c = rotr_nz(a, 37);
+  a += s.w64(8);
+  c += rotr_nz(a, 7);
+  a += s.w64(16);
+  const u64 vf = a + z;
+  const u64 vs = b + rotr_nz(a, 31) + c;
+  a = s.w64(16) + s.w64(n - 32);
+  z = s.w64(n - 8);
+  b = rotr_nz(a + z, 52);
+  c = rotr_nz(a, 37);
+  a += s.w64(n - 24);
+  c += rotr_nz(a, 7);
+  a += s.w64(n - 16);
+  const u64 wf = a + z;
+  const u64 ws = b + rotr_nz(a, 31) + c;
+  const u64 r = smix((vf + ws) * kK2 + (wf + vs) * kK0);
+  return smix(r * kK0 + vs) * kK2;
+}
+
+// 56 bytes of running state of the >64-byte loops (city.c:236-260, :315-350)
+struct LongState {
+  u64 x, y, z;
+  u128 v, w;
+};
+
+// One 64-byte round at byte offset o, including the z<->x exchange
+// (city.c:248-257 == :329-338 == :340-349).
+template <class R>
+PDHT_HD void round64(LongState &st, const R &s, u32 o) {
+  u64 x = rotr_nz(st.x + st.y + st.v.lo + s.w64(o + 8), 37) * kK1;
+  u64 y = rotr_nz(st.y + st.v.hi + s.w64(o + 48), 42) * kK1;
+  x ^= st.w.hi;
+  y += st.v.lo + s.w64(o + 40);
+  const u64 z = rotr_nz(st.z + st.w.lo, 33) * kK1;
+  const u128 v = weak32_at(s, o, st.v.hi * kK1, x + st.w.lo);
+  const u128 w = weak32_at(s, o + 32, z + st.w.hi, y + s.w64(o + 16));
+  st.v = v;
+  st.w = w;
+  st.x = z;
+  st.y = y;
+  st.z = x;
+}
+
+// city.c:224-263
+template <class R>
+PDHT_HD u64 city64(const R &s, u64 len) {
+  if (len <= 32) return len <= 16 ? len0to16(s, len) : len17to32(s, len);
+  if (len <= 64) return len33to64(s, len);
+  const u32 n = (u32)len;
+  LongState st;
+  st.x = s.w64(n - 40);
+  st.y = s.w64(n - 16) + s.w64(n - 56);
+  st.z = mix16(s.w64(n - 48) + len, s.w64(n - 24));
+  st.v = weak32_at(s, n - 64, len, st.z);
+  st.w = weak32_at(s, n - 32, st.y + kK1, st.x);
+  st.x = st.x * kK1 + s.w64(0);
+  const u32 rounds = (u32)((len - 1) >> 6);
+  for (u32 r = 0; r < rounds; ++r) round64(st, s, r << 6);
+  return mix16(mix16(st.v.lo, st.w.lo) + smix(st.y) * kK1 + st.z,
+               mix16(st.v.hi, st.w.hi) + st.x);
+}
+
+// city.c:265-272
+template <class R>
+PDHT_HD u64 city64_seeds(const R &s, u64 len, u64 seed0, u64 seed1) {
+  return mix16(city64(s, len) - seed0, seed1);
+}
+
+// ----------------------------------------------------------- CityHash128 ---
+// city.c:276-308 (CityMurmur), len < 128
+template <class R>
+PDHT_HD u128 murmur128(const R &s, u64 len, u128 seed) {
+  u64 a = seed.lo, b = seed.hi, c, d;
+  if (len <= 16) {
+    a = smix(a * kK1) * kK1;
+    c = b * kK1 + len0to16(s, len);
+    d = smix(a + (len >= 8 ? s.w64(0) : c));
+  } else {
+    const u32 n = (u32)len;
+    c = mix16(s.w64(n - 8) + kK1, a);
+    d = mix16(b + len, c + s.w64(n - 16));
+    a += d;
+    const u32 steps = (n - 1) >> 4;  // signed l = len-16; do..while (l > 0)
+    for (u32 k = 0; k < steps; ++k) {
+      a ^= smix(s.w64(16 * k) * kK1) * kK1;
+      a *= kK1;
+      b ^= a;
+      c ^= smix(s.w64(16 * k + 8) * kK1) * kK1;
+      c *= kK1;
+      d ^= c;
+    }
+  }
+  a = mix16(a, c);
+  b = mix16(d, b);
+  return u128{a ^ b, mix16(b, a)};
+}
+
+// city.c:310-376
+template <class R>
+PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
+  if (len < 128) return murmur128(s, len, seed);
+  LongState st;
+  st.x = seed.lo;
+  st.y = seed.hi;
+  st.z = len * kK1;
+  st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + s.w64(0);
+  st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + s.w64(8);
+  st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
+  st.w.hi = rotr_nz(st.x + s.w64(88), 53) * kK1;
+  u32 o = 0;
+  u64 rem = len;
+  do {
+    round64(st, s, o);
+    round64(st, s, o + 64);
+    o += 128;
+    rem -= 128;
+  } while (rem >= 128);
+  u64 x = st.x, y = st.y, z = st.z;
+  u128 v = st.v, w = st.w;
+  x += rotr_nz(v.lo + z, 49) * kK0;
+  z += rotr_nz(w.lo, 37) * kK0;
+  for (u32 done = 0; done < (u32)rem;) {  // city.c:357-365, tail from the end
+    done += 32;
+    const u32 p = o + (u32)rem - done;
+    y = rotr_nz(x + y, 42) * kK0 + v.hi;
+    w.lo += s.w64(p + 16);
+    x = x * kK0 + w.lo;
+    z += w.hi + s.w64(p);
+    w.hi += v.lo;
+    v = weak32_at(s, p, v.lo + z, v.hi);
+  }
+  x = mix16(x, v.lo);
+  y = mix16(y + z, w.lo);
+  return u128{mix16(x + v.hi, w.hi) + y, mix16(x + w.hi, y + v.hi)};
+}
+
+// city.c:378-400
+template <class R>
+PDHT_HD u128 city128(const R &s, u64 len) {
+  if (len >= 16) {
+    return city128_seed(s.at(16), len - 16, u128{s.w64(0) ^ kK3, s.w64(8)});
+  }
+  if (len >= 8) {
+    // WithSeed(NULL, 0, seed): no key byte is read after the seed is formed
+    const u128 seed{s.w64(0) ^ (len * kK0), s.w64((u32)len - 8) ^ kK1};
+    return murmur128(s, 0, seed);
+  }
+  return murmur128(s, len, u128{kK0, kK1});
+}
+
+// ------------------------------------------------- CRC-32C (long CRC path) ---
+// _mm_crc32_u64 (city.c:435-439): reflected CRC-32C (poly 0x82F63B78) over the
+// 8 little-endian bytes of v, from the low 32 bits of crc, no inversion.
+// Slicing-by-8 tables, built at compile time.
+struct Crc32cTables {
+  u32 t[8][256];
+};
+constexpr Crc32cTables make_crc32c_tables() {
+  Crc32cTables T{};
+  for (u32 i = 0; i < 256; ++i) {
+    u32 c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    T.t[0][i] = c;
+  }
+  for (u32 i = 0; i < 256; ++i)
+    for (int s = 1; s < 8; ++s) T.t[s][i] = (T.t[s - 1][i] >> 8) ^ T.t[0][T.t[s - 1][i] & 0xff];
+  return T;
+}
+
+__device__ __constant__ const Crc32cTables kCrcDev = make_crc32c_tables();
+static constexpr Crc32cTables kCrcHost = make_crc32c_tables();
+
+PDHT_HD u64 crc32c_u64(u64 crc, u64 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const Crc32cTables &T = kCrcDev;
+#else
+  const Crc32cTables &T = kCrcHost;
+#endif
+  const u64 x = v ^ (u32)crc;
+  return T.t[7][x & 0xff] ^ T.t[6][(x >> 8) & 0xff] ^ T.t[5][(x >> 16) & 0xff] ^
+         T.t[4][(x >> 24) & 0xff] ^ T.t[3][(x >> 32) & 0xff] ^ T.t[2][(x >> 40) & 0xff] ^
+         T.t[1][(x >> 48) & 0xff] ^ T.t[0][x >> 56];
+}
+
+// Zero-padded view used by CityHashCrc256Short (city.c:476-481): bytes past
+// `len` of the underlying key read as 0.
+template <class R>
+struct PadReader {
+  R r;
+  u32 len;
+  PDHT_HD u64 w64(u32 o) const {
+    if (o + 8 <= len) return r.w64(o);
+    u64 v = 0;
+    for (u32 i = 0; i < 8; ++i)
+      if (o + i < len) v |= (u64)r.b8(o + i) << (8 * i);
+    return v;
+  }
+  PDHT_HD u32 w32(u32 o) const { return (u32)w64(o); }
+  PDHT_HD u32 b8(u32 o) const { return o < len ? r.b8(o) : 0u; }
+};
+
+// city.c:407-473 (CityHashCrc256Long), len >= 240
+template <class R>
+PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4]) {
+  u64 a = s.w64(56) + kK0;
+  u64 b = s.w64(96) + kK0;
+  u64 c = out[0] = mix16(b, len);
+  u64 d = out[1] = s.w64(120) * kK0 + len;
+  u64 e = s.w64(184) + seed;
+  u64 f = seed, g = 0, h = 0, i = 0, j = 0;
+  u64 t = c + d;
+  u32 o = 0;
+  auto chunk = [&](u64 mult, u32 flip) {
+    const u64 a0 = a;
+    a = rotr(b, 41u ^ flip) * mult + s.w64(o);
+    b = rotr(c, 27u ^ flip) * mult + s.w64(o + 8);
+    c = rotr(d, 41u ^ flip) * mult + s.w64(o + 16);
+    d = rotr(e, 33u ^ flip) * mult + s.w64(o + 24);
+    e = rotr(t, 25u ^ flip) * mult + s.w64(o + 32);
+    t = a0;
+    f = crc32c_u64(f, a);
+    g = crc32c_u64(g, b);
+    h = crc32c_u64(h, c);
+    i = crc32c_u64(i, d);
+    j = crc32c_u64(j, e);
+    o += 40;
+  };
+  const u64 blocks = len / 240;
+  u64 rest = len - blocks * 240;
+  for (u64 k = 0; k < blocks; ++k) {
+    chunk(1, 1);
+    chunk(kK0, 0);
+    chunk(1, 1);
+    chunk(kK0, 0);
+    chunk(1, 1);
+    chunk(kK0, 0);
+  }
+  for (; rest >= 40; rest -= 40) chunk(kK0, 0);
+  if (rest > 0) {
+    o = o + (u32)rest - 40;
+    chunk(kK0, 0);
+  }
+  j += i << 32;
+  a = mix16(a, j);
+  h += g << 32;
+  b += h;
+  c = mix16(c, f) + i;
+  d = mix16(d, e + out[0]);
+  j += e;
+  i += mix16(h, t);
+  e = mix16(a, d) + j;
+  f = mix16(b, c) + a;
+  g = mix16(j, i) + c;
+  out[0] = e + f + g + h;
+  a = smix((a + g) * kK0) * kK0 + b;
+  out[1] += a + out[0];
+  a = smix(a * kK0) * kK0 + c;
+  out[2] = a + out[1];
+  a = smix((a + e) * kK0) * kK0;
+  out[3] = a + out[2];
+}
+
+// city.c:476-489
+template <class R>
+PDHT_HD void crc256(const R &s, u64 len, u64 out[4]) {
+  if (len >= 240) {
+    crc256_long(s, len, 0u, out);
+  } else {
+    crc256_long(PadReader<R>{s, (u32)len}, 240, ~(u32)len, out);
+  }
+}
+
+// city.c:491-504
+template <class R>
+PDHT_HD u128 crc128_seed(const R &s, u64 len, u128 seed) {
+  if (len <= 900) return city128_seed(s, len, seed);
+  u64 r[4];
+  crc256(s, len, r);
+  const u64 u = seed.hi + r[0];
+  const u64 v = seed.lo + r[1];
+  return u128{mix16(u, v + r[2]), mix16(rotr_nz(v, 32), u * kK0 + r[3])};
+}
+
+// city.c:506-517
+template <class R>
+PDHT_HD u128 crc128(const R &s, u64 len) {
+  if (len <= 900) return city128(s, len);
+  u64 r[4];
+  crc256(s, len, r);
+  return u128{r[2], r[3]};
+}
+
+}  // namespace pdht

@@ -1,0 +1,565 @@
+// pdht_hip.hip -- C-ABI of the batch key-hashing engine (include/pdht_hip.h).
+//
+// Launch logic, per-device state, and the host-resident streaming pipeline.
+// Kernels: kernels.h.  Algorithm: city_core.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/pdht_hip.h"
+#include "kernels.h"
+
+#define PDHT_API extern "C" __attribute__((visibility("default")))
+
+namespace pdht {
+
+// ------------------------------------------------------------- errors ---
+static thread_local char g_err[512] = "";
+static thread_local const char *g_kernel = "";
+
+static int fail(const char *fmt, const char *a = "", long long b = 0) {
+  snprintf(g_err, sizeof g_err, fmt, a, b);
+  return PDHT_HIP_ERROR;
+}
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) return fail("%s (" #expr ")", hipGetErrorString(e_)); \
+  } while (0)
+
+static std::atomic<int> g_variant{0};
+
+// ------------------------------------------------------- device state ---
+constexpr int kMaxDev = 64;
+struct DevInfo {
+  std::once_flag once;
+  int cus = 0;
+  hipError_t err = hipSuccess;
+};
+static DevInfo g_dev[kMaxDev];
+
+static int current_device(int *dev) {
+  HIP_TRY(hipGetDevice(dev));
+  if (*dev < 0 || *dev >= kMaxDev) return fail("device index %s%lld out of range", "", *dev);
+  DevInfo &d = g_dev[*dev];
+  std::call_once(d.once, [&] {
+    d.err = hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, *dev);
+  });
+  if (d.err != hipSuccess) return fail("%s (querying CU count)", hipGetErrorString(d.err));
+  return 0;
+}
+
+// Persistent grid: enough workgroups to keep every CU at `per_cu` blocks,
+// never more than the work needs.
+static unsigned grid_for(u64 work_blocks, int per_cu, int dev) {
+  const u64 cap = (u64)std::max(1, g_dev[dev].cus) * per_cu;
+  return (unsigned)std::max<u64>(1, std::min<u64>(work_blocks, cap));
+}
+
+static FastMod make_fastmod(u64 d) {
+  FastMod f{};
+  f.d = d;
+  if ((d & (d - 1)) == 0) {  // includes d == 1 (mask 0)
+    f.pow2 = 1;
+    return f;
+  }
+  u32 l = 64 - __builtin_clzll(d - 1);  // ceil(log2 d), 2..64
+  unsigned __int128 num = ((unsigned __int128)(((unsigned __int128)1 << l) - d)) << 64;
+  f.m = (u64)(num / d) + 1;
+  f.sh = l - 1;
+  f.pow2 = 0;
+  return f;
+}
+
+// --------------------------------------------------------- launchers ---
+constexpr int kWinBytes = 12288;  // LDS window per wave (12 KiB)
+
+// Fixed-length keys: dispatch to the register-direct / LDS-transposed kernel
+// when the length is one of the specialised ones and the layout allows it,
+// else to the generic window kernel.
+template <class Algo, class Sink>
+static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo,
+                        Sink sink, hipStream_t st) {
+  if (n == 0) return 0;
+  if (!keys) return fail("null key pointer%s", "");
+  if (stride < keylen) return fail("stride < keylen%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  const uint8_t *k = static_cast<const uint8_t *>(keys);
+  const bool packed = stride == keylen;
+  const bool al16 = ((uintptr_t)k & 15) == 0;
+  const bool al8 = ((uintptr_t)k & 7) == 0;
+  const int variant = g_variant.load(std::memory_order_relaxed);
+  const u64 blocks = (n + kBlock - 1) / kBlock;
+  if (packed && keylen == 64 && al16 && variant != 3) {
+    if (variant == 2) {
+      g_kernel = "k_fixed_lds64";
+      k_fixed_lds64<Algo, Sink><<<grid_for((n + 255) / 256, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+    } else {
+      g_kernel = "k_fixed_direct<64,1>";
+      k_fixed_direct<64, 1, Algo, Sink><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+    }
+  } else if (packed && keylen == 32 && al16 && variant != 3) {
+    g_kernel = "k_fixed_direct<32,2>";
+    k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+  } else if (packed && keylen == 16 && al16 && variant != 3) {
+    g_kernel = "k_fixed_direct<16,2>";
+    k_fixed_direct<16, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+  } else if (packed && keylen == 8 && al8 && variant != 3) {
+    g_kernel = "k_fixed_direct<8,4>";
+    k_fixed_direct<8, 4, Algo, Sink><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+  } else {
+    g_kernel = "k_window<fixed>";
+    const u64 tiles = (n + 63) / 64;
+    k_window<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+        k, nullptr, 0, stride, keylen, n, algo, sink);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+template <class Algo, class Sink>
+static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
+                      Sink sink, hipStream_t st) {
+  if (n == 0) return 0;
+  if (!bytes || !offsets) return fail("null bytes/offsets pointer%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  g_kernel = "k_window<var>";
+  const u64 tiles = (n + 63) / 64;
+  k_window<kWinBytes, true, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+      static_cast<const uint8_t *>(bytes), offsets, obase, 0, 0, n, algo, sink);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+static SinkPlace make_place_sink(u64 *mbits, u32 *ptindex, void *rank, size_t rank_stride,
+                                 u64 *hist, u32 nptes, u32 nranks) {
+  SinkPlace s{};
+  s.mbits = mbits;
+  s.ptindex = ptindex;
+  s.rank = static_cast<uint8_t *>(rank);
+  s.rank_stride = rank_stride;
+  s.hist = hist;
+  s.pt = make_fastmod(nptes);
+  s.rk = make_fastmod(nranks);
+  s.nranks = nranks;
+  return s;
+}
+
+static int check_place(size_t n, const u64 *mbits, u32 nptes, u32 nranks, const void *rank,
+                       size_t rank_stride) {
+  if (n && !mbits) return fail("mbits must not be NULL%s", "");
+  if (nptes == 0) return fail("nptes must be >= 1 (hash.c:27 divides by it)%s", "");
+  if (nranks == 0) return fail("nranks must be >= 1 (hash.c:29 divides by it)%s", "");
+  if (rank && rank_stride < 4) return fail("rank_stride must be >= 4%s", "");
+  return 0;
+}
+
+// ------------------------------------------------- host-resident path ---
+// Per-device streaming context: NS slots, each with a stream, device
+// buffers and pinned staging, used round-robin so chunk c+1's H2D overlaps
+// chunk c's kernel and chunk c-1's D2H.
+constexpr int kSlots = 3;
+constexpr size_t kChunkBytes = 32u << 20;  // key bytes per chunk
+
+struct Slot {
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t *d_in = nullptr;    // keys (and offsets after them for var)
+  uint8_t *d_out = nullptr;   // digests / placement outputs
+  uint8_t *h_in = nullptr;    // pinned staging (pageable inputs)
+  uint8_t *h_out = nullptr;   // pinned staging (pageable outputs)
+  size_t in_cap = 0, out_cap = 0;
+  // pending harvest of staged outputs
+  struct Copy {
+    void *dst;
+    size_t off, bytes;
+  };
+  std::vector<Copy> pending;
+  bool busy = false;
+};
+struct HostCtx {
+  std::mutex mu;
+  bool ready = false;
+  Slot slot[kSlots];
+};
+static HostCtx g_host[kMaxDev];
+
+static bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+static int slot_reserve(Slot &s, size_t in_bytes, size_t out_bytes) {
+  if (!s.st) HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+  if (!s.done) HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  if (in_bytes > s.in_cap) {
+    if (s.d_in) HIP_TRY(hipFree(s.d_in));
+    if (s.h_in) HIP_TRY(hipHostFree(s.h_in));
+    s.d_in = nullptr;
+    s.h_in = nullptr;
+    HIP_TRY(hipMalloc(&s.d_in, in_bytes));
+    HIP_TRY(hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault));
+    s.in_cap = in_bytes;
+  }
+  if (out_bytes > s.out_cap) {
+    if (s.d_out) HIP_TRY(hipFree(s.d_out));
+    if (s.h_out) HIP_TRY(hipHostFree(s.h_out));
+    s.d_out = nullptr;
+    s.h_out = nullptr;
+    HIP_TRY(hipMalloc(&s.d_out, out_bytes));
+    HIP_TRY(hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault));
+    s.out_cap = out_bytes;
+  }
+  return 0;
+}
+
+// Wait for the slot's previous chunk and copy its staged outputs out.
+static int slot_drain(Slot &s) {
+  if (!s.busy) return 0;
+  HIP_TRY(hipEventSynchronize(s.done));
+  for (auto &c : s.pending) memcpy(c.dst, s.h_out + c.off, c.bytes);
+  s.pending.clear();
+  s.busy = false;
+  return 0;
+}
+
+// One output array of a chunk: device region [doff, doff+bytes) of d_out goes
+// to host `dst` (pinned: DMA directly; pageable: via h_out + harvest).
+static int chunk_out(Slot &s, void *dst, bool pinned, size_t doff, size_t bytes) {
+  if (bytes == 0) return 0;
+  if (pinned) {
+    HIP_TRY(hipMemcpyAsync(dst, s.d_out + doff, bytes, hipMemcpyDeviceToHost, s.st));
+  } else {
+    HIP_TRY(hipMemcpyAsync(s.h_out + doff, s.d_out + doff, bytes, hipMemcpyDeviceToHost, s.st));
+    s.pending.push_back(Slot::Copy{dst, doff, bytes});
+  }
+  return 0;
+}
+
+static int chunk_in(Slot &s, const void *src, bool pinned, size_t doff, size_t bytes) {
+  if (bytes == 0) return 0;
+  const void *from = src;
+  if (!pinned) {
+    memcpy(s.h_in + doff, src, bytes);
+    from = s.h_in + doff;
+  }
+  HIP_TRY(hipMemcpyAsync(s.d_in + doff, from, bytes, hipMemcpyHostToDevice, s.st));
+  return 0;
+}
+
+// Drive a chunked host-resident batch.  `plan(c, &k0, &k1)` yields chunk c's
+// key range (false when done); `run(slot, k0, k1)` stages, launches and
+// queues the copies of one chunk on slot.st.
+template <class Plan, class Run>
+static int host_pipeline(int device, Plan plan, Run run) {
+  if (device < 0 || device >= kMaxDev) return fail("device index %s%lld out of range", "", device);
+  int prev = -1;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(device));
+  HostCtx &H = g_host[device];
+  std::lock_guard<std::mutex> lock(H.mu);
+  int rc = 0;
+  size_t k0, k1;
+  for (size_t c = 0; rc == 0 && plan(c, &k0, &k1); ++c) {
+    Slot &s = H.slot[c % kSlots];
+    rc = slot_drain(s);
+    if (rc == 0) rc = run(s, k0, k1);
+    if (rc == 0) {
+      hipError_t e = hipEventRecord(s.done, s.st);
+      if (e != hipSuccess) rc = fail("%s (hipEventRecord)", hipGetErrorString(e));
+      s.busy = true;
+    }
+  }
+  for (int i = 0; i < kSlots; ++i) {
+    int r2 = slot_drain(H.slot[i]);
+    if (rc == 0) rc = r2;
+  }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+// Fixed-length host batch with a per-chunk device launcher.
+template <class Launch>
+static int host_fixed(const void *keys, size_t keylen, size_t n, size_t out_per_key,
+                      void *out, int device, Launch launch) {
+  if (n == 0) return 0;
+  if (!keys || !out || keylen == 0) return fail("null pointer or zero keylen%s", "");
+  const size_t per = std::max<size_t>(1, kChunkBytes / keylen);
+  const bool pin_in = is_pinned(keys), pin_out = is_pinned(out);
+  auto plan = [&](size_t c, size_t *a, size_t *b) {
+    if (c * per >= n) return false;
+    *a = c * per;
+    *b = std::min(n, *a + per);
+    return true;
+  };
+  auto run = [&](Slot &s, size_t a, size_t b) -> int {
+    const size_t cnt = b - a;
+    if (int rc = slot_reserve(s, per * keylen, per * out_per_key)) return rc;
+    if (int rc = chunk_in(s, static_cast<const uint8_t *>(keys) + a * keylen, pin_in, 0, cnt * keylen))
+      return rc;
+    if (int rc = launch(s.d_in, cnt, s.d_out, s.st)) return rc;
+    return chunk_out(s, static_cast<uint8_t *>(out) + a * out_per_key, pin_out, 0, cnt * out_per_key);
+  };
+  return host_pipeline(device, plan, run);
+}
+
+}  // namespace pdht
+
+using namespace pdht;
+
+// ===================================================================== ABI ===
+PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.1 (gfx950, CityHash v1.0.x)"; }
+PDHT_API const char *pdht_hip_last_error(void) { return g_err; }
+PDHT_API const char *pdht_hip_last_kernel(void) { return g_kernel; }
+PDHT_API int pdht_hip_set_variant(int v) { return g_variant.exchange(v); }
+
+PDHT_API int pdht_hip_device_count(int *count) {
+  if (!count) return fail("null count%s", "");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e == hipErrorNoDevice) {
+    (void)hipGetLastError();
+    c = 0;
+  } else if (e != hipSuccess) {
+    *count = 0;
+    return fail("%s (hipGetDeviceCount)", hipGetErrorString(e));
+  }
+  *count = c;
+  return 0;
+}
+
+PDHT_API int pdht_hip_set_device(int device) {
+  HIP_TRY(hipSetDevice(device));
+  int dev;
+  return current_device(&dev);
+}
+
+#define ST(s) reinterpret_cast<hipStream_t>(s)
+
+PDHT_API int pdht_city64_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
+                                   uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_fixed(keys, stride, keylen, n, AlgoCity64{}, Sink64{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_city64_seeds_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
+                                         uint64_t seed0, uint64_t seed1, uint64_t *out,
+                                         pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_fixed(keys, stride, keylen, n, AlgoCity64Seeds{seed0, seed1}, Sink64{nullptr, out},
+                      ST(s));
+}
+PDHT_API int pdht_city64_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
+                                       uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_var(bytes, offsets, 0, n, AlgoCity64{}, Sink64{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_city128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
+                                    uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_fixed(keys, stride, keylen, n, AlgoCity128{}, Sink128{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_city128_seed_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
+                                         uint64_t lo, uint64_t hi, uint64_t *out,
+                                         pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_fixed(keys, stride, keylen, n, AlgoCity128Seed{lo, hi}, Sink128{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_city128_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
+                                        uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_var(bytes, offsets, 0, n, AlgoCity128{}, Sink128{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
+                                       uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_fixed(keys, stride, keylen, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride, size_t keylen,
+                                            size_t n, uint64_t lo, uint64_t hi, uint64_t *out,
+                                            pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_fixed(keys, stride, keylen, n, AlgoCrc128Seed{lo, hi}, Sink128{nullptr, out}, ST(s));
+}
+PDHT_API int pdht_citycrc128_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
+                                           uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_var(bytes, offsets, 0, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));
+}
+
+PDHT_API int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
+                                  uint32_t nranks, uint64_t *mbits, uint32_t *ptindex, void *rank,
+                                  size_t rank_stride, uint64_t *hist, pdht_hip_stream_t s) {
+  if (int rc = check_place(n, mbits, nptes, nranks, rank, rank_stride)) return rc;
+  return launch_fixed(keys, keysize, keysize, n, AlgoCity64{},
+                      make_place_sink(mbits, ptindex, rank, rank_stride, hist, nptes, nranks), ST(s));
+}
+
+// -------------------------------------------------------- host batches ---
+PDHT_API int pdht_city64_batch_host(const void *keys, size_t keylen, size_t n, uint64_t *out,
+                                    int device) {
+  return host_fixed(keys, keylen, n, 8, out, device,
+                    [&](const uint8_t *dk, size_t cnt, uint8_t *dout, hipStream_t st) {
+                      return launch_fixed(dk, keylen, keylen, cnt, AlgoCity64{},
+                                          Sink64{nullptr, reinterpret_cast<u64 *>(dout)}, st);
+                    });
+}
+
+PDHT_API int pdht_citycrc128_batch_host(const void *keys, size_t keylen, size_t n, uint64_t *out,
+                                        int device) {
+  return host_fixed(keys, keylen, n, 16, out, device,
+                    [&](const uint8_t *dk, size_t cnt, uint8_t *dout, hipStream_t st) {
+                      return launch_fixed(dk, keylen, keylen, cnt, AlgoCrc128{},
+                                          Sink128{nullptr, reinterpret_cast<u64 *>(dout)}, st);
+                    });
+}
+
+PDHT_API int pdht_place_batch_host(const void *keys, size_t keysize, size_t n, uint32_t nptes,
+                                   uint32_t nranks, uint64_t *mbits, uint32_t *ptindex, void *rank,
+                                   size_t rank_stride, int device) {
+  if (int rc = check_place(n, mbits, nptes, nranks, rank, rank_stride)) return rc;
+  if (n == 0) return 0;
+  if (!keys || keysize == 0) return fail("null keys or zero keysize%s", "");
+  const size_t per = std::max<size_t>(1, kChunkBytes / keysize);
+  const bool pin_in = is_pinned(keys);
+  const bool pin_m = is_pinned(mbits);
+  const bool pin_p = ptindex && is_pinned(ptindex);
+  const bool pin_r = rank && is_pinned(rank);
+  // device output layout per chunk: [mbits u64 x per][ptindex u32 x per][rank u32 x per]
+  const size_t o_pt = per * 8, o_rk = per * 12;
+  auto plan = [&](size_t c, size_t *a, size_t *b) {
+    if (c * per >= n) return false;
+    *a = c * per;
+    *b = std::min(n, *a + per);
+    return true;
+  };
+  auto run = [&](Slot &s, size_t a, size_t b) -> int {
+    const size_t cnt = b - a;
+    if (int rc = slot_reserve(s, per * keysize, per * 16)) return rc;
+    if (int rc = chunk_in(s, static_cast<const uint8_t *>(keys) + a * keysize, pin_in, 0, cnt * keysize))
+      return rc;
+    u64 *dm = reinterpret_cast<u64 *>(s.d_out);
+    u32 *dp = ptindex ? reinterpret_cast<u32 *>(s.d_out + o_pt) : nullptr;
+    u32 *dr = rank ? reinterpret_cast<u32 *>(s.d_out + o_rk) : nullptr;
+    if (int rc = launch_fixed(s.d_in, keysize, keysize, cnt, AlgoCity64{},
+                              make_place_sink(dm, dp, dr, 4, nullptr, nptes, nranks), s.st))
+      return rc;
+    if (int rc = chunk_out(s, mbits + a, pin_m, 0, cnt * 8)) return rc;
+    if (ptindex)
+      if (int rc = chunk_out(s, ptindex + a, pin_p, o_pt, cnt * 4)) return rc;
+    if (rank) {
+      if (rank_stride == 4) {
+        if (int rc = chunk_out(s, static_cast<uint32_t *>(rank) + a, pin_r, o_rk, cnt * 4)) return rc;
+      } else {
+        // strided ptl_process_t destination: 2-D copy of the 4-byte members
+        HIP_TRY(hipMemcpy2DAsync(static_cast<uint8_t *>(rank) + a * rank_stride, rank_stride,
+                                 s.d_out + o_rk, 4, 4, cnt, hipMemcpyDeviceToHost, s.st));
+      }
+    }
+    return 0;
+  };
+  return host_pipeline(device, plan, run);
+}
+
+PDHT_API int pdht_city64_batch_var_host(const void *bytes, const uint64_t *offsets, size_t n,
+                                        uint64_t *out, int device) {
+  if (n == 0) return 0;
+  if (!bytes || !offsets || !out) return fail("null pointer%s", "");
+  const bool pin_in = is_pinned(bytes), pin_out = is_pinned(out);
+  const size_t max_keys = kChunkBytes / 16;
+  // chunk c covers keys [a, b) with at most kChunkBytes of key bytes (a key
+  // longer than that gets a chunk of its own and a larger buffer)
+  size_t next = 0;
+  std::vector<std::pair<size_t, size_t>> chunks;
+  while (next < n) {
+    size_t a = next, b = a + 1;
+    const u64 lim = offsets[a] + kChunkBytes;
+    size_t hi = std::min(n, a + max_keys);
+    // largest b <= hi with offsets[b] <= lim (binary search; offsets sorted)
+    size_t lo_b = a + 1, hi_b = hi;
+    while (lo_b < hi_b) {
+      size_t mid = (lo_b + hi_b + 1) / 2;
+      if (offsets[mid] <= lim) lo_b = mid; else hi_b = mid - 1;
+    }
+    b = std::max(a + 1, lo_b);
+    chunks.push_back({a, b});
+    next = b;
+  }
+  auto plan = [&](size_t c, size_t *a, size_t *b) {
+    if (c >= chunks.size()) return false;
+    *a = chunks[c].first;
+    *b = chunks[c].second;
+    return true;
+  };
+  auto run = [&](Slot &s, size_t a, size_t b) -> int {
+    const size_t cnt = b - a;
+    const size_t nbytes = offsets[b] - offsets[a];
+    const size_t off_at = (nbytes + 255) & ~(size_t)255;  // offsets after the bytes
+    if (int rc = slot_reserve(s, std::max(off_at + (max_keys + 1) * 8, off_at + (cnt + 1) * 8),
+                              max_keys * 8))
+      return rc;
+    if (int rc = chunk_in(s, static_cast<const uint8_t *>(bytes) + offsets[a], pin_in, 0, nbytes)) return rc;
+    // offsets are always staged (tiny) so that they can be copied as-is
+    HIP_TRY(hipMemcpyAsync(s.d_in + off_at, offsets + a, (cnt + 1) * 8, hipMemcpyHostToDevice, s.st));
+    if (int rc = launch_var(s.d_in, reinterpret_cast<const u64 *>(s.d_in + off_at), offsets[a], cnt,
+                            AlgoCity64{}, Sink64{nullptr, reinterpret_cast<u64 *>(s.d_out)}, s.st))
+      return rc;
+    return chunk_out(s, out + a, pin_out, 0, cnt * 8);
+  };
+  return host_pipeline(device, plan, run);
+}
+
+// ---------------------------------------------------- synthetic workloads ---
+namespace pdht {
+__device__ __forceinline__ u64 splitmix64_at(u64 seed, u64 k) {
+  u64 z = seed + (k + 1) * 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(kBlock) void k_splitmix64(u64 seed, u64 first, u64 nwords, u64 *out) {
+  const u64 stride = (u64)gridDim.x * kBlock;
+  for (u64 w = (u64)blockIdx.x * kBlock + threadIdx.x; w < nwords; w += stride)
+    out[w] = splitmix64_at(seed, first + w);
+}
+__global__ __launch_bounds__(kBlock) void k_mixed_lengths(u64 seed, u64 first, u64 n, u32 lo,
+                                                          u32 span, u64 *lens) {
+  const u64 stride = (u64)gridDim.x * kBlock;
+  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    lens[i] = lo + splitmix64_at(seed, first + i) % span;
+}
+}  // namespace pdht
+
+PDHT_API int pdht_hip_splitmix64_fill_dev(uint64_t seed, uint64_t first, size_t nwords,
+                                          uint64_t *out, pdht_hip_stream_t s) {
+  if (nwords == 0) return 0;
+  if (!out) return fail("null out%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  k_splitmix64<<<grid_for((nwords + kBlock - 1) / kBlock, 8, dev), kBlock, 0, ST(s)>>>(seed, first,
+                                                                                         nwords, out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+PDHT_API int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n, uint32_t lo,
+                                        uint32_t hi, uint64_t *lens, pdht_hip_stream_t s) {
+  if (n == 0) return 0;
+  if (!lens || hi < lo) return fail("bad arguments%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  k_mixed_lengths<<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, ST(s)>>>(
+      seed, first, n, lo, hi - lo + 1, lens);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors in tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only where /root/reference exists: it compiles the reference
+libpdht/city.c from where it lies (oracle/Makefile -> oracle/_ref/) and calls
+its CityHash64 / CityHash128 / CityHashCrc128 / CityHashCrc256 symbols.  Only
+data (inputs are regenerated from documented patterns; outputs are digests)
+is written; no reference source goes into the repo.
+
+pdht_hash placement (libpdht/hash.c:25-30) cannot be compiled here (pdht.h
+needs portals4.h), so its vectors are the reference CityHash64 digest plus
+the two modulo reductions of hash.c:27 and :29 done in Python.
+
+  python tests/golden/gen_golden.py          # small fixtures (seconds)
+  python tests/golden/gen_golden.py --full   # + full-config fold checksums
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+M = 1 << 20
+
+SEED64 = 0x0123456789ABCDEF
+SEED128 = (0x0F1E2D3C4B5A6978, 0x8796A5B4C3D2E1F0)
+
+
+def pattern_a(n: int) -> bytes:
+    return bytes(i & 0xFF for i in range(n))
+
+
+def pattern_b(n: int) -> bytes:
+    return bytes((i * 7 + 3) & 0xFF for i in range(n))
+
+
+def u128(r) -> tuple[int, int]:
+    return r.first, r.second
+
+
+def small(R) -> dict:
+    out: dict[str, np.ndarray] = {}
+    lens = np.arange(0, 1025, dtype=np.uint64)
+    out["lens"] = lens
+    for tag, pat in (("A", pattern_a), ("B", pattern_b)):
+        buf = pat(1024)
+        c64 = np.empty(1025, np.uint64)
+        c128 = np.empty((1025, 2), np.uint64)
+        crc128 = np.empty((1025, 2), np.uint64)
+        for L in range(1025):
+            c64[L] = R.CityHash64(buf, L)
+            c128[L] = u128(R.CityHash128(buf, L))
+            crc128[L] = u128(R.CityHashCrc128(buf, L))
+        out[f"pat{tag}_city64"] = c64
+        out[f"pat{tag}_city128"] = c128
+        # CityHashCrc128 == CityHash128 for len <= 900 (city.c:492-493, :507-508);
+        # that identity is asserted by the tests, only 901..1024 is stored.
+        assert (crc128[:901] == c128[:901]).all()
+        out[f"pat{tag}_crc128_901up"] = crc128[901:]
+    # seeded variants and CRC-256 on pattern A (city.h:72-84, citycrc.h:39-46)
+    buf = pattern_a(1024)
+    s64 = np.empty(1025, np.uint64)
+    s64s = np.empty(1025, np.uint64)
+    s128 = np.empty((1025, 2), np.uint64)
+    scrc = np.empty((1025, 2), np.uint64)
+    crc256 = np.empty((1025, 4), np.uint64)
+    seed = O.Uint128(*SEED128)
+    for L in range(1025):
+        s64[L] = R.CityHash64WithSeed(buf, L, SEED64)
+        s64s[L] = R.CityHash64WithSeeds(buf, L, SEED128[0], SEED128[1])
+        s128[L] = u128(R.CityHash128WithSeed(buf, L, seed))
+        scrc[L] = u128(R.CityHashCrc128WithSeed(buf, L, seed))
+        r4 = (C.c_uint64 * 4)()
+        R.CityHashCrc256(buf, L, r4)
+        crc256[L] = tuple(r4)
+    out["patA_city64_seed"] = s64
+    out["patA_city64_seeds"] = s64s
+    out["patA_city128_seed"] = s128
+    assert (scrc[:901] == s128[:901]).all()
+    out["patA_crc128_seed_901up"] = scrc[901:]
+    out["patA_crc256"] = crc256
+    out["seed64"] = np.array([SEED64], np.uint64)
+    out["seed128"] = np.array(SEED128, np.uint64)
+    # long keys (CRC-256 long path, CityHash128 long loop)
+    long_lens = np.array([1500, 2047, 2048, 4096, 10007], np.uint64)
+    lb = pattern_b(int(long_lens.max()))
+    out["long_lens"] = long_lens
+    out["longB_city64"] = np.array([R.CityHash64(lb, int(L)) for L in long_lens], np.uint64)
+    out["longB_city128"] = np.array([u128(R.CityHash128(lb, int(L))) for L in long_lens], np.uint64)
+    out["longB_crc128"] = np.array([u128(R.CityHashCrc128(lb, int(L))) for L in long_lens], np.uint64)
+    # splitmix64 stream head (pins the synthetic-key generator)
+    out["splitmix_head"] = O.splitmix64(O.SEED_KEYS, 0, 64)
+    out["splitmix_lens_head"] = O.splitmix64(O.SEED_LENS, 0, 64)
+    # 1024 random 64-byte keys (the cfg2 workload's first keys)
+    k64 = O.fixed_keys(1024, 64)
+    out["rand64_city64"] = O.apply_ref64(k64, 1024, L=64, fn_name="CityHash64")
+    out["rand64_city128"] = O.apply_ref128(k64, 1024, L=64, fn_name="CityHash128")
+    assert (O.apply_ref128(k64, 1024, L=64, fn_name="CityHashCrc128") == out["rand64_city128"]).all()
+    # 1024 mixed 16..256-byte keys (the cfg3 workload's first keys)
+    data, offs = O.mixed_keys(1024)
+    out["mixed_offsets"] = offs
+    out["mixed_city64"] = O.apply_ref64(data, 1024, offsets=offs)
+    out["mixed_city128"] = O.apply_ref128(data, 1024, offsets=offs, fn_name="CityHash128")
+    assert (O.apply_ref128(data, 1024, offsets=offs, fn_name="CityHashCrc128")
+            == out["mixed_city128"]).all()
+    # pdht_hash on `unsigned long` keys 0..255 (test/scaling.c:137 key type)
+    keys = np.arange(256, dtype=np.uint64).view(np.uint8).reshape(256, 8)
+    mb = O.apply_ref64(keys, 256, L=8)
+    out["pdht_u64keys_mbits"] = mb
+    nptes = [1, 2, 3, 8]
+    nranks = [1, 2, 3, 4, 7, 8, 64, 1000, 65537]
+    out["pdht_nptes"] = np.array(nptes, np.uint64)
+    out["pdht_nranks"] = np.array(nranks, np.uint64)
+    out["pdht_ptindex"] = np.stack([(mb % np.uint64(p)).astype(np.uint32) for p in nptes])
+    out["pdht_rank"] = np.stack([(mb % np.uint64(r)).astype(np.uint32) for r in nranks])
+    return out
+
+
+def folds_full(R) -> dict:
+    """Fold checksums (sum d_i*(2i+1) mod 2^64) of the full BASELINE configs,
+    per 1/8 shard so every world size 1/2/4/8 can check its own slice."""
+    res = {}
+    thr = os.cpu_count() or 8
+
+    def fixed_fold(n, L, fn, name, shards=8, is128=False):
+        per = n // shards
+        parts = []
+        chunk = 16 * M
+        for s in range(shards):
+            acc = 0
+            for k0 in range(s * per, (s + 1) * per, chunk):
+                cnt = min(chunk, (s + 1) * per - k0)
+                keys = O.fixed_keys(cnt, L, first_key=k0)
+                if is128:
+                    d = O.apply_ref128(keys, cnt, L=L, threads=thr, fn_name=fn)
+                    # fold over the interleaved {lo,hi} array, index 2i and 2i+1
+                    acc = (acc + O.fold64(d.reshape(-1), 2 * k0)) % (1 << 64)
+                else:
+                    d = O.apply_ref64(keys, cnt, L=L, threads=thr, fn_name=fn)
+                    acc = (acc + O.fold64(d, k0)) % (1 << 64)
+            parts.append(acc)
+            print(f"  {name} shard {s}: {acc:016x}", flush=True)
+        res[name] = {"n": n, "L": L, "shards": [f"{p:016x}" for p in parts],
+                     "total": f"{sum(parts) % (1 << 64):016x}"}
+
+    fixed_fold(1 * M, 64, "CityHash64", "cfg1_city64_1M_x64", shards=1)
+    fixed_fold(16 * M, 64, "CityHash64", "cfg2_city64_16M_x64")
+    fixed_fold(16 * M, 64, "CityHashCrc128", "cfg4_crc128_16M_x64", is128=True)
+    # cfg3: 64M mixed 16..256 B keys
+    n = 64 * M
+    data, offs = O.mixed_keys(n)
+    d = O.apply_ref64(data, n, offsets=offs, threads=thr)
+    per = n // 8
+    parts = [O.fold64(d[s * per:(s + 1) * per], s * per) for s in range(8)]
+    res["cfg3_city64_64M_mixed"] = {"n": n, "lo": 16, "hi": 256, "total_bytes": int(offs[-1]),
+                                    "shards": [f"{p:016x}" for p in parts],
+                                    "total": f"{sum(parts) % (1 << 64):016x}"}
+    del data, offs, d
+    fixed_fold(1 << 30, 64, "CityHash64", "cfg5_city64_1B_x64")
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--full", action="store_true")
+    a = ap.parse_args()
+    O.build()
+    R = O.ref()
+    if R is None:
+        sys.exit("oracle/_ref not built: /root/reference is required to regenerate fixtures")
+    vec = small(R)
+    np.savez_compressed(os.path.join(HERE, "city_golden.npz"), **vec)
+    print("wrote city_golden.npz", os.path.getsize(os.path.join(HERE, "city_golden.npz")), "bytes")
+    if a.full:
+        res = folds_full(R)
+        with open(os.path.join(HERE, "config_folds.json"), "w") as f:
+            json.dump({"generator": "tests/golden/gen_golden.py --full (reference city.c via oracle/_ref)",
+                       "key_seed": f"{O.SEED_KEYS:016x}", "len_seed": f"{O.SEED_LENS:016x}",
+                       "fold": "sum_i d_i*(2i+1) mod 2^64 over global key index i "
+                               "(128-bit digests: over the interleaved lo,hi array)",
+                       "configs": res}, f, indent=1)
+        print("wrote config_folds.json")
+
+
+if __name__ == "__main__":
+    main()

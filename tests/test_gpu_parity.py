@@ -1,0 +1,282 @@
+"""GPU parity: the HIP kernels against the oracle and the reference golden data.
+
+Bit-exact everywhere (integer hashing).  Small/medium cases compare every
+digest with the oracle (oracle/city_oracle.c, itself pinned to the compiled
+reference city.c); the full BASELINE configs compare position-weighted fold
+checksums with tests/golden/config_folds.json (generated from the reference).
+All calls go through the C-ABI (pdht_amd -> libpdht_hip.so).
+"""
+import numpy as np
+import pytest
+
+from conftest import pattern_a
+
+torch = pytest.importorskip("torch")
+import pdht_amd as P  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+M = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def gpu_fold(d, first_index=0):
+    """sum_i d_i * (2(first+i)+1) mod 2^64 on the GPU (int64 wraps)."""
+    d = d.reshape(-1)
+    idx = torch.arange(d.numel(), device=d.device, dtype=torch.int64) + first_index
+    return int((d * (2 * idx + 1)).sum().item()) & 0xFFFFFFFFFFFFFFFF
+
+
+def device_keys(n, L, first_key=0, dev="cuda"):
+    """The BASELINE synthetic keys (splitmix64 byte stream), generated on device."""
+    assert (first_key * L) % 8 == 0 and (n * L) % 8 == 0
+    w = P.splitmix64_fill(0x5EED5EED5EED5EED, first_key * L // 8, n * L // 8, device=dev)
+    return w.view(torch.uint8).view(n, L)
+
+
+# ------------------------------------------------------------- fixed keys ---
+def test_generator_matches_oracle(dev, oracle):
+    w = P.splitmix64_fill(oracle.SEED_KEYS, 5, 1000, device=dev)
+    assert (u64(w) == oracle.splitmix64(oracle.SEED_KEYS, 5, 1000)).all()
+    lens = P.mixed_lengths(oracle.SEED_LENS, 0, 5000, 16, 256, device=dev)
+    assert (lens.cpu().numpy().astype(np.uint64) == oracle.mixed_lengths(5000)).all()
+
+
+@pytest.mark.parametrize("L", list(range(0, 300)) + [511, 512, 899, 900, 901, 1000, 2047, 4097])
+def test_city64_every_length(dev, oracle, L):
+    rng = np.random.default_rng(L)
+    n = 131  # two full waves + a ragged one
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    got = u64(P.city64_batch(to_dev(k, dev)))
+    assert (got == oracle.city64_fixed(k)).all()
+    if L in (8, 16, 32, 64):
+        assert P.last_kernel().startswith("k_fixed_direct"), P.last_kernel()
+    else:
+        assert P.last_kernel() == "k_window<fixed>"
+
+
+@pytest.mark.parametrize("L", [0, 1, 3, 8, 13, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 144, 200, 901, 2000])
+def test_city128_crc128_lengths(dev, oracle, L):
+    rng = np.random.default_rng(1000 + L)
+    n = 70
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    assert (u64(P.city128_batch(kd)) == oracle.city128_fixed(k)).all()
+    assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
+
+
+@pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 300, 1200])
+def test_seeded_batches(dev, oracle, L):
+    rng = np.random.default_rng(77 + L)
+    k = rng.integers(0, 256, (65, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
+    got = u64(P.city64_seeds_batch(kd, s0, s1))
+    assert [int(x) for x in got] == [oracle.city64_seeds(r.tobytes(), s0, s1) for r in k]
+    got = u64(P.city64_seed_batch(kd, s1))
+    assert [int(x) for x in got] == [oracle.city64_seed(r.tobytes(), s1) for r in k]
+    got = u64(P.city128_seed_batch(kd, (s0, s1))).reshape(-1, 2)
+    assert [tuple(int(x) for x in g) for g in got] == [oracle.city128_seed(r.tobytes(), s0, s1) for r in k]
+    got = u64(P.citycrc128_seed_batch(kd, (s0, s1))).reshape(-1, 2)
+    assert [tuple(int(x) for x in g) for g in got] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k]
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_64B_kernel_variants_bitexact(dev, oracle, variant):
+    n = M + 13
+    k = oracle.fixed_keys(n, 64)
+    want = oracle.city64_fixed(k)
+    kd = to_dev(k, dev)
+    old = P.set_variant(variant)
+    try:
+        got = u64(P.city64_batch(kd))
+        kern = P.last_kernel()
+        got128 = u64(P.citycrc128_batch(kd[:100000]))
+    finally:
+        P.set_variant(old)
+    assert kern == {1: "k_fixed_direct<64,1>", 2: "k_fixed_lds64", 3: "k_window<fixed>"}[variant]
+    assert (got == want).all()
+    assert (got128 == oracle.city128_fixed(k[:100000], crc=True)).all()
+
+
+def test_golden_random_64B(dev, golden, oracle):
+    kd = device_keys(1024, 64, dev=dev)
+    assert (u64(P.city64_batch(kd)) == golden["rand64_city64"]).all()
+    assert (u64(P.citycrc128_batch(kd)) == golden["rand64_city128"]).all()
+    assert (u64(P.city128_batch(kd)) == golden["rand64_city128"]).all()
+
+
+def test_edge_layouts(dev, oracle):
+    rng = np.random.default_rng(5)
+    # n = 0 and n = 1
+    z = torch.empty((0, 64), dtype=torch.uint8, device=dev)
+    assert P.city64_batch(z).numel() == 0
+    k1 = rng.integers(0, 256, (1, 64), dtype=np.uint8)
+    assert int(u64(P.city64_batch(to_dev(k1, dev)))[0]) == oracle.city64(k1[0].tobytes())
+    # strided rows (stride 80, keylen 64) and a 1-byte-misaligned base
+    big = rng.integers(0, 256, (1000, 80), dtype=np.uint8)
+    bd = to_dev(big, dev)
+    got = u64(P.city64_batch(bd[:, :64]))
+    assert P.last_kernel() == "k_window<fixed>"
+    assert (got == oracle.city64_fixed(big[:, :64])).all()
+    flat = to_dev(rng.integers(0, 256, 64 * 777 + 1, dtype=np.uint8), dev)
+    mis = flat[1:].view(777, 64)
+    got = u64(P.city64_batch(mis))
+    assert (got == oracle.city64_fixed(mis.cpu().numpy())).all()
+
+
+def test_errors_are_loud(dev):
+    k = torch.zeros((4, 8), dtype=torch.uint8, device=dev)
+    with pytest.raises(P.PdhtError):
+        P.place_batch(k, nptes=0, nranks=1)
+    with pytest.raises(P.PdhtError):
+        P.place_batch(k, nptes=1, nranks=0)
+
+
+# ---------------------------------------------------------- variable keys ---
+def test_var_golden_mixed(dev, golden, oracle):
+    data, offs = oracle.mixed_keys(1024)
+    dd, od = to_dev(data, dev), to_dev(offs.astype(np.int64), dev)
+    assert (u64(P.city64_var_batch(dd, od)) == golden["mixed_city64"]).all()
+    assert (u64(P.city128_var_batch(dd, od)) == golden["mixed_city128"]).all()
+    assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
+
+
+def test_var_edge_cases(dev, oracle):
+    rng = np.random.default_rng(9)
+    # empty keys, 1..3-byte keys, keys far longer than the LDS window, all mixed
+    lens = np.concatenate([np.zeros(40, np.int64), rng.integers(0, 40, 300),
+                           rng.integers(0, 300, 300), [0, 20000, 1, 50000, 13000, 0],
+                           rng.integers(800, 1100, 50)])
+    rng.shuffle(lens)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    data = rng.integers(0, 256, int(offs[-1]) + 3, dtype=np.uint8)
+    # misaligned base: hash data[3:] with the same offsets
+    for base in (0, 3):
+        d = data[base:base + int(offs[-1])]
+        dd = to_dev(d, dev)
+        od = to_dev(offs.astype(np.int64), dev)
+        assert (u64(P.city64_var_batch(dd, od)) == oracle.city64_var(d, offs)).all()
+        assert (u64(P.city128_var_batch(dd, od)) == oracle.city128_var(d, offs)).all()
+        assert (u64(P.citycrc128_var_batch(dd, od)) == oracle.city128_var(d, offs, crc=True)).all()
+
+
+def test_var_1M_mixed(dev, oracle):
+    data, offs = oracle.mixed_keys(M)
+    dd, od = to_dev(data, dev), to_dev(offs.astype(np.int64), dev)
+    assert (u64(P.city64_var_batch(dd, od)) == oracle.city64_var(data, offs)).all()
+
+
+# ---------------------------------------------------- fused placement ---
+@pytest.mark.parametrize("L", [8, 13, 32, 64])
+@pytest.mark.parametrize("nptes,nranks", [(1, 1), (3, 7), (8, 64), (5, 1000), (2, 4096), (7, 4097),
+                                          (0xFFFFFFFF, 0xFFFFFFFB), (0x80000000, 65537)])
+def test_place_batch(dev, oracle, L, nptes, nranks):
+    rng = np.random.default_rng(L * 31 + nranks)
+    n = 5000
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    hist = torch.zeros(nranks, dtype=torch.int64, device=dev)
+    mb, pt, rk = P.place_batch(to_dev(k, dev), nptes, nranks, hist=hist)
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, nptes, nranks)
+    assert (u64(mb) == m2).all()
+    assert (pt.cpu().numpy().view(np.uint32) == p2).all()
+    assert (rk.cpu().numpy().view(np.uint32) == r2).all()
+    assert (hist.cpu().numpy() == np.bincount(r2, minlength=nranks)).all()
+
+
+def test_place_golden_u64_keys(dev, golden):
+    keys = np.arange(256, dtype=np.uint64).view(np.uint8).reshape(256, 8)
+    kd = to_dev(keys, dev)
+    for a, p in enumerate(golden["pdht_nptes"]):
+        for b, r in enumerate(golden["pdht_nranks"]):
+            mb, pt, rk = P.place_batch(kd, int(p), int(r))
+            assert (u64(mb) == golden["pdht_u64keys_mbits"]).all()
+            assert (pt.cpu().numpy().view(np.uint32) == golden["pdht_ptindex"][a]).all()
+            assert (rk.cpu().numpy().view(np.uint32) == golden["pdht_rank"][b]).all()
+
+
+# -------------------------------------------------------- host-resident ---
+def test_host_resident_paths(dev, oracle):
+    n = 2 * M + 5  # > 1 chunk of the pipeline (32 MiB of keys)
+    k = oracle.fixed_keys(n, 64)
+    want = oracle.city64_fixed(k)
+    assert (P.city64_batch_host(k) == want).all()  # pageable: staged
+    kp = torch.from_numpy(k).pin_memory()
+    op = torch.empty(n, dtype=torch.int64).pin_memory()
+    P.city64_batch_host(kp, out=op)  # pinned: direct DMA
+    assert (op.numpy().view(np.uint64) == want).all()
+    assert (P.citycrc128_batch_host(k[:300000]) == oracle.city128_fixed(k[:300000], crc=True)).all()
+    data, offs = oracle.mixed_keys(600000)
+    assert (P.city64_var_batch_host(data, offs) == oracle.city64_var(data, offs)).all()
+    k8 = oracle.fixed_keys(100000, 8)
+    mb, pt, rk = P.place_batch_host(k8, 3, 12)
+    m2, p2, r2 = oracle.pdht_hash_fixed(k8, 3, 12)
+    assert (mb == m2).all() and (pt == p2).all() and (rk == r2).all()
+
+
+def test_pdht_hash_batch_default_and_plugin(dev, oracle):
+    t = P.PdhtTable(keysize=13, nptes=4, nranks=10)
+    k = oracle.fixed_keys(5000, 13)
+    mb, pt, rk = t.hash_batch(k)  # default hash -> GPU, ptl_process_t stride 8
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 4, 10)
+    assert (mb == m2).all() and (pt == p2).all() and (rk == r2).all()
+    # scalar pdht_hash agrees with the batch
+    for i in (0, 1, 4999):
+        assert t.hash(k[i].tobytes()) == (int(m2[i]), int(p2[i]), int(r2[i]))
+
+
+# --------------------------------------------------- full BASELINE configs ---
+def test_cfg2_16M_x64_full_fold(dev, folds):
+    f = folds["cfg2_city64_16M_x64"]
+    kd = device_keys(f["n"], 64, dev=dev)
+    for variant in (1, 2):
+        old = P.set_variant(variant)
+        try:
+            d = P.city64_batch(kd)
+        finally:
+            P.set_variant(old)
+        assert f"{gpu_fold(d):016x}" == f["total"], variant
+
+
+def test_cfg4_crc128_16M_full_fold(dev, folds):
+    f = folds["cfg4_crc128_16M_x64"]
+    kd = device_keys(f["n"], 64, dev=dev)
+    d = P.citycrc128_batch(kd)
+    assert f"{gpu_fold(d):016x}" == f["total"]
+
+
+def test_cfg3_64M_mixed_full_fold(dev, folds):
+    f = folds["cfg3_city64_64M_mixed"]
+    n = f["n"]
+    lens = P.mixed_lengths(0x1E575EED1E575EED, 0, n, 16, 256, device=dev)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item())
+    assert total == f["total_bytes"]
+    words = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, (total + 7) // 8, device=dev)
+    data = words.view(torch.uint8)[:total]
+    d = P.city64_var_batch(data, offs)
+    assert f"{gpu_fold(d):016x}" == f["total"]
+
+
+def test_cfg5_shard0_of_1B(dev, folds):
+    """Shard 0 of the 8-GPU 1B-key config (keys [0, 128M)) on this GPU."""
+    f = folds["cfg5_city64_1B_x64"]
+    per = f["n"] // 8
+    kd = device_keys(per, 64, dev=dev)
+    d = P.city64_batch(kd)
+    assert f"{gpu_fold(d, 0):016x}" == f["shards"][0]
