@@ -153,6 +153,20 @@ def main():
     else:
         kern_ms_max = kern_ms
 
+    # -------------------------------------------- achievable read stream ---
+    calib = None
+    if cfg in ("cfg2", "cfg4"):
+        P.read_stream(keys, True)
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(10)]
+        for s, e in cev:
+            s.record()
+            P.read_stream(keys, True)
+            e.record()
+        torch.cuda.synchronize()
+        cms = float(np.median([s.elapsed_time(e) for s, e in cev]))
+        calib = round(n * L / (cms / 1e3) / 1e9, 1)
+
     # ------------------------------------------------------------ parity ---
     parity = check_parity(P, torch, cfg, rank, world, n, first, out, locals())
     if world > 1:
@@ -186,7 +200,8 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
                      "traffic": load_traffic(cfg, n), "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
-                     "read_only_GBps": round(total_bytes_in / (kern_ms / 1e3) / 1e9, 1)},
+                     "read_only_GBps": round(total_bytes_in / (kern_ms / 1e3) / 1e9, 1),
+                     "calibrated_read_stream_GBps": calib},
         "parity": parity,
     }
     if rank == 0 and world == 1 and cfg in ("cfg2", "cfg4") and not a.no_host:

@@ -133,6 +133,12 @@ int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
 int pdht_hip_set_variant(int variant);
 /* Name of the kernel the last batch call on this thread launched. */
 const char *pdht_hip_last_kernel(void);
+/* HBM calibration: stream `bytes` (multiple of 16, 16-B aligned) through a
+ * read-only kernel with 16-B coalesced loads (nt != 0: non-temporal) and
+ * XOR-fold them into *out (one uint64, device).  Gives the achievable read
+ * bandwidth the hash kernels are compared with. */
+int pdht_hip_read_stream_dev(const void *buf, size_t bytes, int nt, uint64_t *out,
+                             pdht_hip_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -99,6 +99,7 @@ def _declare(L):
         "pdht_place_batch_host": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _V, _V, _S, C.c_int]),
         "pdht_hip_splitmix64_fill_dev": (C.c_int, [_U64, _U64, _S, _V, _V]),
         "pdht_hip_mixed_lengths_dev": (C.c_int, [_U64, _U64, _S, _U32, _U32, _V, _V]),
+        "pdht_hip_read_stream_dev": (C.c_int, [_V, _S, C.c_int, _V, _V]),
         "CityHash64": (_U64, [_V, _S]),
         "CityHash64WithSeed": (_U64, [_V, _S, _U64]),
         "CityHash64WithSeeds": (_U64, [_V, _S, _U64, _U64]),
@@ -228,9 +229,9 @@ def _keys_2d(keys):
     torch = _torch()
     if keys.dtype != torch.uint8 or keys.dim() != 2 or not keys.is_cuda:
         raise ValueError("keys must be a CUDA uint8 tensor of shape [n, keylen]")
-    if keys.stride(1) != 1:
-        raise ValueError("keys rows must be contiguous")
     n, L = keys.shape
+    if keys.stride(1) != 1 and L > 1 and n > 0:
+        raise ValueError("keys rows must be contiguous")
     stride = keys.stride(0) if n > 1 else L
     return n, L, stride
 
@@ -361,6 +362,16 @@ def splitmix64_fill(seed: int, first: int, nwords: int, out=None, device="cuda",
         out = torch.empty(nwords, dtype=torch.int64, device=device)
     _check(lib().pdht_hip_splitmix64_fill_dev(seed, first, nwords, _dptr(out), _stream_ptr(stream)),
            "pdht_hip_splitmix64_fill_dev")
+    return out
+
+
+def read_stream(buf, nt: bool = False, out=None, stream=None):
+    """HBM read-bandwidth calibration: XOR-fold of a CUDA buffer (16-B multiple)."""
+    torch = _torch()
+    if out is None:
+        out = torch.zeros(1, dtype=torch.int64, device=buf.device)
+    _check(lib().pdht_hip_read_stream_dev(_dptr(buf), buf.numel() * buf.element_size(), int(nt),
+                                          _dptr(out), _stream_ptr(stream)), "pdht_hip_read_stream_dev")
     return out
 
 

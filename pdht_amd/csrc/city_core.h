@@ -53,8 +53,8 @@ PDHT_HD u64 mix16(u64 u, u64 v) {
 }
 
 // ---------------------------------------------------------------- readers ---
-// A reader R exposes: u64 w64(u32 off), u32 w32(u32 off), u32 b8(u32 off)
-// and R at(u32 off) (a reader re-based `off` bytes further).
+// A reader R exposes: u64 w64(u32 off), u32 w32(u32 off), u32 b8(u32 off).
+// Re-based views are Shifted<R> (below).
 
 struct HostReader {
   const uint8_t *p;
@@ -90,11 +90,17 @@ struct RegReader {
   }
   PDHT_HD u32 w32(u32 o) const { return dw(o + base); }
   PDHT_HD u32 b8(u32 o) const { return (dw(o + base)) & 0xffu; }
-  PDHT_HD RegReader at(u32 o) const {
-    RegReader r = *this;
-    r.base += o;
-    return r;
-  }
+};
+
+// A view `off` bytes into another reader.  Holds a reference, never a copy:
+// copying a RegReader's register array would force it into scratch memory.
+template <class R>
+struct Shifted {
+  const R &r;
+  u32 off;
+  PDHT_HD u64 w64(u32 o) const { return r.w64(o + off); }
+  PDHT_HD u32 w32(u32 o) const { return r.w32(o + off); }
+  PDHT_HD u32 b8(u32 o) const { return r.b8(o + off); }
 };
 
 // ----------------------------------------------------------- CityHash64 ---
@@ -293,7 +299,7 @@ PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
 template <class R>
 PDHT_HD u128 city128(const R &s, u64 len) {
   if (len >= 16) {
-    return city128_seed(s.at(16), len - 16, u128{s.w64(0) ^ kK3, s.w64(8)});
+    return city128_seed(Shifted<R>{s, 16}, len - 16, u128{s.w64(0) ^ kK3, s.w64(8)});
   }
   if (len >= 8) {
     // WithSeed(NULL, 0, seed): no key byte is read after the seed is formed
@@ -341,7 +347,7 @@ PDHT_HD u64 crc32c_u64(u64 crc, u64 v) {
 // `len` of the underlying key read as 0.
 template <class R>
 struct PadReader {
-  R r;
+  const R &r;
   u32 len;
   PDHT_HD u64 w64(u32 o) const {
     if (o + 8 <= len) return r.w64(o);

@@ -109,15 +109,26 @@ struct AlgoCrc128Seed {
 // ----------------------------------------------------------------- sinks ---
 // Where a digest goes.  init()/flush() run once per workgroup around the
 // grid-stride loop (every thread reaches both).
-struct Sink64 {
+template <bool NT, class T>
+__device__ __forceinline__ void st(T v, T *p) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+// NTS: non-temporal digest stores (cache-policy experiment knob).
+template <bool NTS = false>
+struct Sink64T {
   static constexpr u32 kHist = 1;  // LDS histogram words this sink needs
   u32 *lds_hist;
   u64 *out;
   __device__ __forceinline__ void init() {}
-  __device__ __forceinline__ void put(u64 i, u64 h) { __builtin_nontemporal_store(h, out + i); }
+  __device__ __forceinline__ void put(u64 i, u64 h) { st<NTS>(h, out + i); }
   __device__ __forceinline__ void flush() {}
 };
-struct Sink128 {
+template <bool NTS = false>
+struct Sink128T {
   static constexpr u32 kHist = 1;
   u32 *lds_hist;
   u64 *out;
@@ -125,9 +136,28 @@ struct Sink128 {
   __device__ __forceinline__ void put(u64 i, u128 h) {
     typedef u64 u64x2 __attribute__((ext_vector_type(2)));
     u64x2 v = {h.lo, h.hi};
-    __builtin_nontemporal_store(v, reinterpret_cast<u64x2 *>(out) + i);
+    st<NTS>(v, reinterpret_cast<u64x2 *>(out) + i);
   }
   __device__ __forceinline__ void flush() {}
+};
+typedef Sink64T<false> Sink64;
+typedef Sink128T<false> Sink128;
+
+// The same sink with non-temporal stores (identity for other sinks).
+template <class S>
+struct NtSink {
+  typedef S type;
+  static __device__ __host__ S make(S s) { return s; }
+};
+template <>
+struct NtSink<Sink64> {
+  typedef Sink64T<true> type;
+  static __host__ type make(Sink64 s) { return type{s.lds_hist, s.out}; }
+};
+template <>
+struct NtSink<Sink128> {
+  typedef Sink128T<true> type;
+  static __host__ type make(Sink128 s) { return type{s.lds_hist, s.out}; }
 };
 
 // u64 remainder by a run-time invariant divisor: Granlund & Montgomery
@@ -165,8 +195,8 @@ struct SinkPlace {
     }
   }
   __device__ __forceinline__ void put(u64 i, u64 h) {
-    __builtin_nontemporal_store(h, mbits + i);
-    if (ptindex) __builtin_nontemporal_store((u32)pt.mod(h), ptindex + i);
+    mbits[i] = h;
+    if (ptindex) ptindex[i] = (u32)pt.mod(h);
     if (rank || hist) {
       const u32 r = (u32)rk.mod(h);
       if (rank) *reinterpret_cast<u32 *>(rank + i * rank_stride) = r;
@@ -188,21 +218,30 @@ struct SinkPlace {
 };
 
 // ------------------------------------------------------------ key loads ---
-template <int L>
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT, class T>
+__device__ __forceinline__ T ld(const T *p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+template <int L, bool NT = false>
 __device__ __forceinline__ void load_key_regs(const uint8_t *__restrict__ keys, u64 i,
                                               RegReader<L / 4> &r) {
   static_assert(L == 8 || L % 16 == 0, "direct path: L = 8 or a multiple of 16");
   if constexpr (L == 8) {
     typedef u32 u32x2 __attribute__((ext_vector_type(2)));
-    const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(keys) + i);
+    const u32x2 v = ld<NT>(reinterpret_cast<const u32x2 *>(keys) + i);
     r.d[0] = v.x;
     r.d[1] = v.y;
   } else {
-    typedef u32 u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 *p = reinterpret_cast<const u32x4 *>(keys + i * (u64)L);
 #pragma unroll
     for (int j = 0; j < L / 16; ++j) {
-      const u32x4 v = __builtin_nontemporal_load(p + j);
+      const u32x4 v = ld<NT>(p + j);
       r.d[4 * j + 0] = v.x;
       r.d[4 * j + 1] = v.y;
       r.d[4 * j + 2] = v.z;
@@ -214,7 +253,7 @@ __device__ __forceinline__ void load_key_regs(const uint8_t *__restrict__ keys, 
 
 // ------------------------------------------------------- direct kernel ---
 // U keys per lane per iteration (all loads issued before any hashing).
-template <int L, int U, class Algo, class Sink>
+template <int L, int U, class Algo, class Sink, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_fixed_direct(const uint8_t *__restrict__ keys, u64 n,
                                                          Algo algo, Sink sink) {
   __shared__ u32 lds_hist[Sink::kHist];
@@ -225,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_direct(const uint8_t *__restri
     RegReader<L / 4> r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i + u * stride < n) load_key_regs<L>(keys, i + u * stride, r[u]);
+      if (i + u * stride < n) load_key_regs<L, NT>(keys, i + u * stride, r[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (i + u * stride < n) sink.put(i + u * stride, algo(r[u], (u64)L));
@@ -234,13 +273,47 @@ __global__ __launch_bounds__(kBlock) void k_fixed_direct(const uint8_t *__restri
 }
 
 // -------------------------------------------------- LDS-transposed 64 B ---
-// A wave's 64 keys (4 KiB) arrive by 4 LDS-DMA instructions: instruction j
-// moves bytes [1024j, 1024j+1024) of the tile, lane l's 16 B landing at
-// LDS byte 1024j + 16l (linear).  Key k's chunk c (16 B) therefore sits at
-// slot 4k + c.  Lane k reads its 4 chunks with ds_read_b128; to keep the
-// 16-lane groups of ds_read_b128 conflict-free the SOURCE is permuted so the
-// image holds chunk c of key k at slot 4k + (c ^ ((k >> 2) & 3)) (the read
-// applies the same involution).
+// A wave's 64 keys (one contiguous 4 KiB tile) are brought in as fully
+// contiguous 1 KiB pieces (piece j = bytes [1024j, 1024j+1024), lane l's
+// 16 B = chunk g = 64j + l = key g>>2, quarter g&3) and transposed through a
+// per-wave LDS image so each lane ends up with its own 64-byte key in VGPRs.
+// Image slot of (key k, quarter c) = 4k + (c ^ ((k >> 2) & 3)): the XOR keeps
+// the 16-lane groups of ds_read_b128 (row reads, lane = key) and the 8-lane
+// groups of ds_write_b128 conflict-free.
+__device__ __forceinline__ u32 xpose_slot(u32 k, u32 c) { return 4 * k + (c ^ ((k >> 2) & 3)); }
+
+// LDS byte address of a __shared__ object (for hand-issued ds_* / M0).
+template <class T>
+__device__ __forceinline__ u32 lds_addr(const T *p) {
+  return (u32)(uintptr_t)(const __attribute__((address_space(3))) T *)(p);
+}
+
+// Row read of lane `lane`'s key from an image at LDS byte address `img`,
+// hand-issued so the compiler does not tie it to outstanding LDS-DMA (it
+// would otherwise wait vmcnt(0) on every DMA in flight, prefetch included).
+__device__ __forceinline__ void read_row_asm(u32 img, u32 lane, RegReader<16> &r) {
+  const u32 sw = (lane >> 2) & 3;
+  u32x4 v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const u32 a = img + 16 * (4 * lane + (c ^ sw));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v[c]) : "v"(a) : "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    r.d[4 * c + 0] = v[c].x;
+    r.d[4 * c + 1] = v[c].y;
+    r.d[4 * c + 2] = v[c].z;
+    r.d[4 * c + 3] = v[c].w;
+  }
+  r.base = 0;
+}
+
+// Variant "lds": pieces arrive by LDS-DMA (global_load_lds_dwordx4, no VGPR
+// staging); the SOURCE address is permuted so that the linear DMA image is
+// the swizzled one; the next tile's DMA is in flight while this one hashes.
 template <class Algo, class Sink>
 __global__ __launch_bounds__(kBlock) void k_fixed_lds64(const uint8_t *__restrict__ keys, u64 n,
                                                         Algo algo, Sink sink) {
@@ -251,19 +324,16 @@ __global__ __launch_bounds__(kBlock) void k_fixed_lds64(const uint8_t *__restric
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lane = threadIdx.x & 63;
   const u64 ntiles = (n + 63) >> 6;
+  const u64 full = n >> 6;  // tiles with 64 valid keys (DMA path)
   const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
-  // DMA of tile t into buffer b (only full tiles; the ragged last tile is
-  // loaded through registers below).
   auto issue = [&](u64 t, int b) {
     const uint8_t *base = keys + (t << 12);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const u32 slot = 64 * j + lane;              // image slot written by this lane
-      const u32 k = slot >> 2, c = slot & 3;        // image holds chunk c ^ swz(k) of key k
-      const u32 src_chunk = c ^ ((k >> 2) & 3);
-      const uint8_t *src = base + k * 64 + src_chunk * 16;
+      const u32 g = 64 * j + lane;               // image slot this lane fills
+      const u32 k = g >> 2, cq = g & 3;            // slot holds quarter cq ^ swz(k) of key k
+      const uint8_t *src = base + k * 64 + ((cq ^ ((k >> 2) & 3)) << 4);
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)src,
                                        (void __attribute__((address_space(3))) *)&tile[wave][b][256 * j],
                                        16, 0, 0);
@@ -271,37 +341,85 @@ __global__ __launch_bounds__(kBlock) void k_fixed_lds64(const uint8_t *__restric
   };
 
   u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
-  const u64 full = n >> 6;  // tiles with 64 valid keys
   int b = 0;
   if (t < full) issue(t, 0);
   for (; t < ntiles; t += nwaves) {
     const u64 tn = t + nwaves;
-    if (tn < full) issue(tn, b ^ 1);  // prefetch next tile into the other buffer
     const u64 i = (t << 6) + lane;
     RegReader<16> r;
     r.base = 0;
     if (t < full) {
-      // wait for this tile's 4 DMAs (the next tile's 4 may stay in flight)
-      if (tn < full)
+      if (tn < full) {
+        issue(tn, b ^ 1);  // next tile streams in while this one hashes
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else
+      } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const u32x4 *row = reinterpret_cast<const u32x4 *>(&tile[wave][b][0]) + 4 * lane;
-      const u32 sw = (lane >> 2) & 3;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const u32x4 v = row[c ^ sw];
-        r.d[4 * c + 0] = v.x;
-        r.d[4 * c + 1] = v.y;
-        r.d[4 * c + 2] = v.z;
-        r.d[4 * c + 3] = v.w;
       }
+      read_row_asm(lds_addr(&tile[wave][b][0]), lane, r);
     } else if (i < n) {
       load_key_regs<64>(keys, i, r);
     }
     if (i < n) sink.put(i, algo(r, (u64)64));
     b ^= 1;
-    __builtin_amdgcn_wave_barrier();  // all lanes done reading buffer b before it is refilled
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sink.flush();
+}
+
+// Variant "xpose": the same transpose with register staging: each lane loads
+// 4 contiguous 16-B pieces of the NEXT tile (global_load_dwordx4, 1 KiB per
+// wave-instruction) while the current tile hashes, then writes them into the
+// image with ds_write_b128.
+template <class Algo, class Sink, bool LNT = false>
+__global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restrict__ keys, u64 n,
+                                                          Algo algo, Sink sink) {
+  __shared__ __attribute__((aligned(16))) u32x4 img[kWavesPerBlock][256];  // 4 KiB per wave
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 full = n >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32x4 pre[4];
+  auto fetch = [&](u64 t) {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(keys + (t << 12));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pre[j] = ld<LNT>(src + 64 * j + lane);
+  };
+  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
+  if (t < full) fetch(t);
+  for (; t < ntiles; t += nwaves) {
+    const u64 tn = t + nwaves;
+    const u64 i = (t << 6) + lane;
+    RegReader<16> r;
+    r.base = 0;
+    if (t < full) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32 g = 64 * j + lane;
+        img[wave][xpose_slot(g >> 2, g & 3)] = pre[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (tn < full) fetch(tn);
+      const u32 sw = (lane >> 2) & 3;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const u32x4 v = img[wave][4 * lane + (c ^ sw)];
+        r.d[4 * c + 0] = v.x;
+        r.d[4 * c + 1] = v.y;
+        r.d[4 * c + 2] = v.z;
+        r.d[4 * c + 3] = v.w;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else if (i < n) {
+      load_key_regs<64>(keys, i, r);
+    }
+    if (i < n) sink.put(i, algo(r, (u64)64));
   }
   sink.flush();
 }

@@ -56,7 +56,13 @@ static int current_device(int *dev) {
 
 // Persistent grid: enough workgroups to keep every CU at `per_cu` blocks,
 // never more than the work needs.
+static int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
 static unsigned grid_for(u64 work_blocks, int per_cu, int dev) {
+  const int ovr = env_int("PDHT_HIP_BLOCKS_PER_CU", 0);  // tuning experiments only
+  if (ovr > 0) per_cu = ovr;
   const u64 cap = (u64)std::max(1, g_dev[dev].cus) * per_cu;
   return (unsigned)std::max<u64>(1, std::min<u64>(work_blocks, cap));
 }
@@ -86,7 +92,7 @@ template <class Algo, class Sink>
 static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo,
                         Sink sink, hipStream_t st) {
   if (n == 0) return 0;
-  if (!keys) return fail("null key pointer%s", "");
+  if (!keys && keylen) return fail("null key pointer%s", "");  // empty keys read nothing
   if (stride < keylen) return fail("stride < keylen%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
@@ -97,12 +103,46 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
   const int variant = g_variant.load(std::memory_order_relaxed);
   const u64 blocks = (n + kBlock - 1) / kBlock;
   if (packed && keylen == 64 && al16 && variant != 3) {
-    if (variant == 2) {
-      g_kernel = "k_fixed_lds64";
-      k_fixed_lds64<Algo, Sink><<<grid_for((n + 255) / 256, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
-    } else {
-      g_kernel = "k_fixed_direct<64,1>";
-      k_fixed_direct<64, 1, Algo, Sink><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+    typedef typename NtSink<Sink>::type SinkNt;
+    const SinkNt sink_nt = NtSink<Sink>::make(sink);
+    const unsigned g1 = grid_for(blocks, 8, dev), g4 = grid_for((n + 255) / 256, 4, dev);
+    switch (variant) {
+      case 2:
+        g_kernel = "k_fixed_lds64";
+        k_fixed_lds64<Algo, Sink><<<g4, kBlock, 0, st>>>(k, n, algo, sink);
+        break;
+      case 4:
+        g_kernel = "k_fixed_lds64<nt-store>";
+        k_fixed_lds64<Algo, SinkNt><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
+      case 5:
+        g_kernel = "k_fixed_direct<64,1,nt-load,nt-store>";
+        k_fixed_direct<64, 1, Algo, SinkNt, true><<<g1, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
+      case 6:
+        g_kernel = "k_fixed_direct<64,1>";
+        k_fixed_direct<64, 1, Algo, Sink, false><<<g1, kBlock, 0, st>>>(k, n, algo, sink);
+        break;
+      case 7:
+        g_kernel = "k_fixed_xpose64<nt-load,nt-store>";
+        k_fixed_xpose64<Algo, SinkNt, true><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
+      case 8:
+        g_kernel = "k_fixed_xpose64<nt-store>";
+        k_fixed_xpose64<Algo, SinkNt, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
+      case 9:
+        g_kernel = "k_fixed_direct<64,1,nt-store>";
+        k_fixed_direct<64, 1, Algo, SinkNt, false><<<g1, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
+      case 1:
+        g_kernel = "k_fixed_xpose64<plain>";
+        k_fixed_xpose64<Algo, Sink, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink);
+        break;
+      default:  // 0: measured fastest (tools/kbench.py)
+        g_kernel = "k_fixed_xpose64";
+        k_fixed_xpose64<Algo, SinkNt, true><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
     }
   } else if (packed && keylen == 32 && al16 && variant != 3) {
     g_kernel = "k_fixed_direct<32,2>";
@@ -157,6 +197,7 @@ static int check_place(size_t n, const u64 *mbits, u32 nptes, u32 nranks, const 
   if (n && !mbits) return fail("mbits must not be NULL%s", "");
   if (nptes == 0) return fail("nptes must be >= 1 (hash.c:27 divides by it)%s", "");
   if (nranks == 0) return fail("nranks must be >= 1 (hash.c:29 divides by it)%s", "");
+  if (nranks > 0x7fffffffu) return fail("nranks is c->size, an int: must be < 2^31%s", "");
   if (rank && rank_stride < 4) return fail("rank_stride must be >= 4%s", "");
   return 0;
 }
@@ -538,7 +579,46 @@ __global__ __launch_bounds__(kBlock) void k_mixed_lengths(u64 seed, u64 first, u
   for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
     lens[i] = lo + splitmix64_at(seed, first + i) % span;
 }
+
+// Read-only HBM stream (calibration), the same access shape as the hash
+// kernels: a wave owns a contiguous 4 KiB tile = 4 wave-instructions of 1 KiB
+// (16 B per lane); grid-stride over tiles; one atomic per wave.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_read_stream(const u32x4 *__restrict__ p, u64 n16,
+                                                        u64 *out) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 wave = (u64)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  const u64 full = n16 >> 8;  // whole 4 KiB tiles
+  u32x4 acc = {0, 0, 0, 0};
+  for (u64 t = wave; t < full; t += nwaves) {
+    const u32x4 *q = p + (t << 8) + lane;
+    const u32x4 a = ld<NT>(q), b = ld<NT>(q + 64), c = ld<NT>(q + 128), d = ld<NT>(q + 192);
+    acc ^= a ^ b ^ c ^ d;
+  }
+  for (u64 i = (full << 8) + wave * 64 + lane; i < n16; i += nwaves * 64) acc ^= ld<NT>(p + i);
+  u64 v = ((u64)(acc.x ^ acc.z) << 32) | (acc.y ^ acc.w);
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned long long *>(out), v);
+}
 }  // namespace pdht
+
+PDHT_API int pdht_hip_read_stream_dev(const void *buf, size_t bytes, int nt, uint64_t *out,
+                                      pdht_hip_stream_t s) {
+  if (bytes == 0) return 0;
+  if (!buf || !out || (bytes & 15) || ((uintptr_t)buf & 15)) return fail("bad buffer%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  const u64 n16 = bytes / 16;
+  const unsigned g = grid_for(((n16 >> 8) + kWavesPerBlock) / kWavesPerBlock, 8, dev);
+  const u32x4 *p = static_cast<const u32x4 *>(buf);
+  if (nt)
+    k_read_stream<true><<<g, kBlock, 0, ST(s)>>>(p, n16, out);
+  else
+    k_read_stream<false><<<g, kBlock, 0, ST(s)>>>(p, n16, out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
 
 PDHT_API int pdht_hip_splitmix64_fill_dev(uint64_t seed, uint64_t first, size_t nwords,
                                           uint64_t *out, pdht_hip_stream_t s) {

@@ -63,7 +63,7 @@ def test_city64_every_length(dev, oracle, L):
     got = u64(P.city64_batch(to_dev(k, dev)))
     assert (got == oracle.city64_fixed(k)).all()
     if L in (8, 16, 32, 64):
-        assert P.last_kernel().startswith("k_fixed_direct"), P.last_kernel()
+        assert P.last_kernel().startswith("k_fixed_"), P.last_kernel()
     else:
         assert P.last_kernel() == "k_window<fixed>"
 
@@ -94,7 +94,14 @@ def test_seeded_batches(dev, oracle, L):
     assert [tuple(int(x) for x in g) for g in got] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+VARIANT_KERNELS = {0: "k_fixed_xpose64", 1: "k_fixed_xpose64<plain>", 2: "k_fixed_lds64",
+                   3: "k_window<fixed>",
+                   4: "k_fixed_lds64<nt-store>", 5: "k_fixed_direct<64,1,nt-load,nt-store>",
+                   6: "k_fixed_direct<64,1>", 7: "k_fixed_xpose64<nt-load,nt-store>",
+                   8: "k_fixed_xpose64<nt-store>", 9: "k_fixed_direct<64,1,nt-store>"}
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANT_KERNELS))
 def test_64B_kernel_variants_bitexact(dev, oracle, variant):
     n = M + 13
     k = oracle.fixed_keys(n, 64)
@@ -107,7 +114,7 @@ def test_64B_kernel_variants_bitexact(dev, oracle, variant):
         got128 = u64(P.citycrc128_batch(kd[:100000]))
     finally:
         P.set_variant(old)
-    assert kern == {1: "k_fixed_direct<64,1>", 2: "k_fixed_lds64", 3: "k_window<fixed>"}[variant]
+    assert kern == VARIANT_KERNELS[variant]
     assert (got == want).all()
     assert (got128 == oracle.city128_fixed(k[:100000], crc=True)).all()
 
@@ -136,6 +143,19 @@ def test_edge_layouts(dev, oracle):
     mis = flat[1:].view(777, 64)
     got = u64(P.city64_batch(mis))
     assert (got == oracle.city64_fixed(mis.cpu().numpy())).all()
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096, 4096 * 1000 + 48])
+def test_read_stream_calibration_kernel(dev, nbytes):
+    rng = np.random.default_rng(nbytes)
+    a = rng.integers(0, 2**63, nbytes // 8, dtype=np.uint64)
+    # the kernel XOR-folds every 16-B piece {x,y,z,w} into (x^z) << 32 | (y^w)
+    d32 = a.view(np.uint32).reshape(-1, 4)
+    x = np.bitwise_xor.reduce(d32[:, 0] ^ d32[:, 2])
+    y = np.bitwise_xor.reduce(d32[:, 1] ^ d32[:, 3])
+    for nt in (False, True):
+        got = int(P.read_stream(to_dev(a.view(np.int64), dev), nt).item()) & 0xFFFFFFFFFFFFFFFF
+        assert got == (int(x) << 32) | int(y)
 
 
 def test_errors_are_loud(dev):
@@ -184,18 +204,21 @@ def test_var_1M_mixed(dev, oracle):
 # ---------------------------------------------------- fused placement ---
 @pytest.mark.parametrize("L", [8, 13, 32, 64])
 @pytest.mark.parametrize("nptes,nranks", [(1, 1), (3, 7), (8, 64), (5, 1000), (2, 4096), (7, 4097),
-                                          (0xFFFFFFFF, 0xFFFFFFFB), (0x80000000, 65537)])
+                                          (0xFFFFFFFF, 0x7FFFFFFF), (0x80000000, 65537),
+                                          (0xFFFFFFFB, 0x7FFFFFED)])
 def test_place_batch(dev, oracle, L, nptes, nranks):
+    # nranks is c->size, a positive int (hash.c:29): the largest is 2^31-1
     rng = np.random.default_rng(L * 31 + nranks)
     n = 5000
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
-    hist = torch.zeros(nranks, dtype=torch.int64, device=dev)
+    hist = torch.zeros(nranks, dtype=torch.int64, device=dev) if nranks <= 1 << 20 else None
     mb, pt, rk = P.place_batch(to_dev(k, dev), nptes, nranks, hist=hist)
     m2, p2, r2 = oracle.pdht_hash_fixed(k, nptes, nranks)
     assert (u64(mb) == m2).all()
     assert (pt.cpu().numpy().view(np.uint32) == p2).all()
     assert (rk.cpu().numpy().view(np.uint32) == r2).all()
-    assert (hist.cpu().numpy() == np.bincount(r2, minlength=nranks)).all()
+    if hist is not None:
+        assert (hist.cpu().numpy() == np.bincount(r2, minlength=nranks)).all()
 
 
 def test_place_golden_u64_keys(dev, golden):

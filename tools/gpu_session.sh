@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session on the box: each step under its own timeout; stop at the
+# first step that crashes (rc > 1) so nothing else touches a faulted GPU.
+#   tools/gpu_session.sh tests smoke bench kbench kbench_crc prof
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+    tests)   timeout -k 10 700 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?
+             tail -4 gpurun_out/gpu_tests.log ;;
+    smoke)   timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+             tail -1 gpurun_out/smoke.log ;;
+    bench)   timeout -k 10 240 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
+             tail -1 gpurun_out/bench.log ;;
+    bench_*) cfg=${step#bench_}; timeout -k 10 300 python bench.py --config $cfg --no-cpu-baseline > gpurun_out/bench_$cfg.log 2>&1; rc=$?
+             tail -1 gpurun_out/bench_$cfg.log ;;
+    kbench)  timeout -k 10 300 python tools/kbench.py > gpurun_out/kbench.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/kbench.log | cut -c1-200 ;;
+    kbench_crc) timeout -k 10 300 python tools/kbench.py --algo crc128 > gpurun_out/kbench_crc.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/kbench_crc.log | cut -c1-200 ;;
+    prof)    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host > gpurun_out/prof.log 2>&1; rc=$?
+             head -3 gpurun_out/prof/run_kernel_stats.csv | cut -c1-200 ;;
+    pmc)     rc=0
+             for ctr in FETCH_SIZE WRITE_SIZE; do
+               timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$ctr" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/pmc_$ctr.log 2>&1 || { rc=$?; break; }
+             done ;;
+    *) echo "unknown step $step"; rc=0 ;;
+  esac
+  echo "[step $step rc=$rc]"
+  [ $rc -le 1 ] || exit $rc
+done
