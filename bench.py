@@ -99,6 +99,7 @@ def main():
             workload = "cfg4: CityHashCrc128 over 16M x 64B keys per GPU, device-resident"
         else:
             hist = torch.zeros(1024, dtype=torch.int64, device=dev)
+            out = None
             step = lambda: P.place_batch(keys, 1, 1024, ptindex=True, rank=True, hist=hist)  # noqa: E731
             bytes_per_key = 8 + 8 + 4 + 4
             workload = "place: fused pdht_hash (mbits+ptindex+rank+hist) over 16M x 8B keys per GPU"

@@ -1,16 +1,19 @@
 // city_core.h -- CityHash v1.0.x arithmetic, written once for host and gfx950.
 //
-// Product code (not the oracle).  Every function is __host__ __device__ and
-// templated on a *reader*: the object that supplies little-endian words of
-// the key at byte offsets.  The same algorithm body is therefore compiled for
-//   * the scalar host API (HostReader: plain memory)          -> city_host.cpp
-//   * fixed-length keys held in VGPRs (RegReader<L>)           -> kernels
-//   * keys staged in LDS at arbitrary byte offsets (LdsReader) -> kernels
-//   * keys read straight from global memory (GlobalReader)     -> kernels
-// With a compile-time length (RegReader<L>) the length dispatch, every byte
-// offset and every rotate amount fold to constants, so the 64-byte path is
-// straight-line VALU over 16 registers.
-//
+// Product code (not the oracle).  Every routine is __host__ __device__ and
+// templated on a *reader*, the object that delivers key bytes.  Readers hand
+// out SPANS: span<N>(o) returns bytes [o, o+N) of the key as a Words<N/4>
+// register array (little-endian dwords) in ONE batched load, and all further
+// word extraction uses compile-time offsets into that array.  CityHash only
+// ever reads 8/16/32/40/64-byte windows at run-time positions (city.c:138-263,
+// :276-400, :407-473), so the algorithm is written in those windows:
+//   * HostReader    -- the scalar host API (memcpy)              city_host.hip
+//   * RegReader<W>  -- fixed-length keys already in VGPRs; with a constant
+//                      length every window folds to register renaming
+//   * LdsReader     -- keys in an LDS window at arbitrary byte offsets: one
+//                      run of dword reads + v_alignbyte_b32 per window
+//   * GlobalReader  -- the same straight from global memory (keys that do not
+//                      fit the LDS window)
 // Behaviour follows /root/reference/libpdht/city.c; each routine cites the
 // lines whose semantics it reproduces.  Parity: tests/ (oracle + golden).
 #pragma once
@@ -38,9 +41,8 @@ constexpr u64 kK3 = 0xc949d7c7509e6557ULL;
 constexpr u64 kMul = 0x9ddfea08eb382d69ULL;
 
 // ---------------------------------------------------------------- bit ops ---
-// city.c:115-125.  `s` is 1..63 at every call site except the runtime rotate
-// of HashLen0to16 (9..16) -- both covered by rotr_nz; rotr keeps the shift-0
-// guard of Rotate() for the generic callers.
+// city.c:115-125.  rotr_nz needs 1 <= s <= 63 (every call site but the
+// CRC-256 chunk, which keeps the shift-0 guard of Rotate() through rotr).
 PDHT_HD u64 rotr_nz(u64 v, u32 s) { return (v >> s) | (v << (64 - s)); }
 PDHT_HD u64 rotr(u64 v, u32 s) { return s == 0 ? v : rotr_nz(v, s); }
 PDHT_HD u64 smix(u64 v) { return v ^ (v >> 47); }  // city.c:127-129
@@ -52,16 +54,25 @@ PDHT_HD u64 mix16(u64 u, u64 v) {
   return b * kMul;
 }
 
-// ---------------------------------------------------------------- readers ---
-// A reader R exposes: u64 w64(u32 off), u32 w32(u32 off), u32 b8(u32 off).
-// Re-based views are Shifted<R> (below).
+// ------------------------------------------------------------ key windows ---
+// W dwords of key bytes in registers; offsets are compile-time constants.
+template <int W>
+struct Words {
+  u32 d[W];
+  PDHT_HD u64 w64(u32 b) const { return ((u64)d[(b >> 2) + 1] << 32) | d[b >> 2]; }
+  PDHT_HD u32 w32(u32 b) const { return d[b >> 2]; }
+};
 
+// ---------------------------------------------------------------- readers ---
+// A reader R exposes  template <int N> Words<N/4> span(off),  u32 w32(off)
+// and u32 b8(off) (the <= 8-byte paths).
 struct HostReader {
   const uint8_t *p;
-  PDHT_HD u64 w64(size_t o) const {
-    u64 r;
-    memcpy(&r, p + o, 8);
-    return r;
+  template <int N>
+  PDHT_HD Words<N / 4> span(size_t o) const {
+    Words<N / 4> w;
+    memcpy(w.d, p + o, N);
+    return w;
   }
   PDHT_HD u32 w32(size_t o) const {
     u32 r;
@@ -69,27 +80,28 @@ struct HostReader {
     return r;
   }
   PDHT_HD u32 b8(size_t o) const { return p[o]; }
-  PDHT_HD HostReader at(size_t o) const { return HostReader{p + o}; }
 };
 
-// Key bytes held in registers as W little-endian dwords; offsets are expected
-// to be compile-time constants after inlining (fixed-length kernels).
+// Key bytes held in registers as W little-endian dwords (fixed-length
+// kernels); offsets are constants after inlining.
 template <int W>
 struct RegReader {
   u32 d[W];
-  u32 base;  // byte offset of this view inside d (compile-time constant)
-  PDHT_HD u32 dw(u32 byte_off) const {  // dword at any byte offset
-    const u32 q = byte_off >> 2, r = byte_off & 3;
+  PDHT_HD u32 dw(u32 b) const {  // dword at any byte offset
+    const u32 q = b >> 2, r = b & 3;
     if (r == 0) return d[q];
     const u32 hi = (q + 1 < (u32)W) ? d[q + 1] : 0u;
     return (u32)((((u64)hi << 32) | d[q]) >> (8 * r));
   }
-  PDHT_HD u64 w64(u32 o) const {
-    o += base;
-    return ((u64)dw(o + 4) << 32) | dw(o);
+  template <int N>
+  PDHT_HD Words<N / 4> span(u32 o) const {
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) w.d[j] = dw(o + 4 * j);
+    return w;
   }
-  PDHT_HD u32 w32(u32 o) const { return dw(o + base); }
-  PDHT_HD u32 b8(u32 o) const { return (dw(o + base)) & 0xffu; }
+  PDHT_HD u32 w32(u32 o) const { return dw(o); }
+  PDHT_HD u32 b8(u32 o) const { return dw(o) & 0xffu; }
 };
 
 // A view `off` bytes into another reader.  Holds a reference, never a copy:
@@ -98,46 +110,79 @@ template <class R>
 struct Shifted {
   const R &r;
   u32 off;
-  PDHT_HD u64 w64(u32 o) const { return r.w64(o + off); }
+  template <int N>
+  PDHT_HD Words<N / 4> span(u32 o) const {
+    return r.template span<N>(o + off);
+  }
   PDHT_HD u32 w32(u32 o) const { return r.w32(o + off); }
   PDHT_HD u32 b8(u32 o) const { return r.b8(o + off); }
 };
+
+// Zero-padded view used by CityHashCrc256Short (city.c:476-481): bytes past
+// `len` of the underlying key read as 0.
+template <class R>
+struct PadReader {
+  const R &r;
+  u32 len;
+  template <int N>
+  PDHT_HD Words<N / 4> span(u32 o) const {
+    if (o + N <= len) return r.template span<N>(o);
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) {
+      u32 v = 0;
+      for (u32 i = 0; i < 4; ++i)
+        if (o + 4 * j + i < len) v |= r.b8(o + 4 * j + i) << (8 * i);
+      w.d[j] = v;
+    }
+    return w;
+  }
+  PDHT_HD u32 w32(u32 o) const { return span<4>(o).d[0]; }
+  PDHT_HD u32 b8(u32 o) const { return o < len ? r.b8(o) : 0u; }
+};
+
+template <class R>
+PDHT_HD u64 fetch64(const R &s, u32 o) {
+  return s.template span<8>(o).w64(0);
+}
 
 // ----------------------------------------------------------- CityHash64 ---
 // city.c:138-157
 template <class R>
 PDHT_HD u64 len0to16(const R &s, u64 len) {
+  const u32 n = (u32)len;
   if (len > 8) {
-    const u64 a = s.w64(0);
-    const u64 b = s.w64((u32)len - 8);
-    return mix16(a, rotr_nz(b + len, (u32)len)) ^ b;
+    const u64 a = fetch64(s, 0);
+    const u64 b = fetch64(s, n - 8);
+    return mix16(a, rotr_nz(b + len, n)) ^ b;
   }
   if (len >= 4) {
     const u64 a = s.w32(0);
-    return mix16(len + (a << 3), (u64)s.w32((u32)len - 4));
+    return mix16(len + (a << 3), (u64)s.w32(n - 4));
   }
   if (len > 0) {
-    const u32 a = s.b8(0), b = s.b8((u32)len >> 1), c = s.b8((u32)len - 1);
+    const u32 a = s.b8(0), b = s.b8(n >> 1), c = s.b8(n - 1);
     const u32 y = a + (b << 8);
-    const u32 z = (u32)len + (c << 2);
+    const u32 z = n + (c << 2);
     return smix((u64)y * kK2 ^ (u64)z * kK3) * kK2;
   }
   return kK2;
 }
 
-// city.c:161-168
+// city.c:161-168 (head = bytes [0,16), tail = bytes [len-16, len))
 template <class R>
 PDHT_HD u64 len17to32(const R &s, u64 len) {
-  const u32 n = (u32)len;
-  const u64 a = s.w64(0) * kK1;
-  const u64 b = s.w64(8);
-  const u64 c = s.w64(n - 8) * kK2;
-  const u64 d = s.w64(n - 16) * kK0;
+  const Words<4> h = s.template span<16>(0);
+  const Words<4> t = s.template span<16>((u32)len - 16);
+  const u64 a = h.w64(0) * kK1;
+  const u64 b = h.w64(8);
+  const u64 c = t.w64(8) * kK2;
+  const u64 d = t.w64(0) * kK0;
   return mix16(rotr_nz(a - b, 43) + rotr_nz(c, 30) + d,
                a + rotr_nz(b ^ kK3, 20) - c + len);
 }
 
-// city.c:173-198 -- WeakHashLen32WithSeeds over four given words
+// city.c:173-198 -- WeakHashLen32WithSeeds
 PDHT_HD u128 weak32(u64 w, u64 x, u64 y, u64 z, u64 a, u64 b) {
   a += w;
   b = rotr_nz(b + a + z, 21);
@@ -147,31 +192,32 @@ PDHT_HD u128 weak32(u64 w, u64 x, u64 y, u64 z, u64 a, u64 b) {
   b += rotr_nz(a, 44);
   return u128{a + z, b + c};
 }
-template <class R>
-PDHT_HD u128 weak32_at(const R &s, u32 o, u64 a, u64 b) {
-  return weak32(s.w64(o), s.w64(o + 8), s.w64(o + 16), s.w64(o + 24), a, b);
+template <int W>
+PDHT_HD u128 weak32_at(const Words<W> &c, u32 o, u64 a, u64 b) {
+  return weak32(c.w64(o), c.w64(o + 8), c.w64(o + 16), c.w64(o + 24), a, b);
 }
 
-// city.c:201-222 -- the 33..64-byte path (the 64-byte key hot path)
+// city.c:201-222 -- 33..64 bytes (head = [0,32), tail = [len-32, len))
 template <class R>
 PDHT_HD u64 len33to64(const R &s, u64 len) {
-  const u32 n = (u32)len;
-  u64 z = s.w64(24);
-  u64 a = s.w64(0) + (len + s.w64(n - 16)) * kK0;
+  const Words<8> h = s.template span<32>(0);
+  const Words<8> t = s.template span<32>((u32)len - 32);
+  u64 z = h.w64(24);
+  u64 a = h.w64(0) + (len + t.w64(16)) * kK0;
   u64 b = rotr_nz(a + z, 52);
   u64 c = rotr_nz(a, 37);
-  a += s.w64(8);
+  a += h.w64(8);
   c += rotr_nz(a, 7);
-  a += s.w64(16);
+  a += h.w64(16);
   const u64 vf = a + z;
   const u64 vs = b + rotr_nz(a, 31) + c;
-  a = s.w64(16) + s.w64(n - 32);
-  z = s.w64(n - 8);
+  a = h.w64(16) + t.w64(0);
+  z = t.w64(24);
   b = rotr_nz(a + z, 52);
   c = rotr_nz(a, 37);
-  a += s.w64(n - 24);
+  a += t.w64(8);
   c += rotr_nz(a, 7);
-  a += s.w64(n - 16);
+  a += t.w64(16);
   const u64 wf = a + z;
   const u64 ws = b + rotr_nz(a, 31) + c;
   const u64 r = smix((vf + ws) * kK2 + (wf + vs) * kK0);
@@ -184,17 +230,16 @@ struct LongState {
   u128 v, w;
 };
 
-// One 64-byte round at byte offset o, including the z<->x exchange
+// One 64-byte round over chunk c, including the z<->x exchange
 // (city.c:248-257 == :329-338 == :340-349).
-template <class R>
-PDHT_HD void round64(LongState &st, const R &s, u32 o) {
-  u64 x = rotr_nz(st.x + st.y + st.v.lo + s.w64(o + 8), 37) * kK1;
-  u64 y = rotr_nz(st.y + st.v.hi + s.w64(o + 48), 42) * kK1;
+PDHT_HD void round64(LongState &st, const Words<16> &c) {
+  u64 x = rotr_nz(st.x + st.y + st.v.lo + c.w64(8), 37) * kK1;
+  u64 y = rotr_nz(st.y + st.v.hi + c.w64(48), 42) * kK1;
   x ^= st.w.hi;
-  y += st.v.lo + s.w64(o + 40);
+  y += st.v.lo + c.w64(40);
   const u64 z = rotr_nz(st.z + st.w.lo, 33) * kK1;
-  const u128 v = weak32_at(s, o, st.v.hi * kK1, x + st.w.lo);
-  const u128 w = weak32_at(s, o + 32, z + st.w.hi, y + s.w64(o + 16));
+  const u128 v = weak32_at(c, 0, st.v.hi * kK1, x + st.w.lo);
+  const u128 w = weak32_at(c, 32, z + st.w.hi, y + c.w64(16));
   st.v = v;
   st.w = w;
   st.x = z;
@@ -209,14 +254,17 @@ PDHT_HD u64 city64(const R &s, u64 len) {
   if (len <= 64) return len33to64(s, len);
   const u32 n = (u32)len;
   LongState st;
-  st.x = s.w64(n - 40);
-  st.y = s.w64(n - 16) + s.w64(n - 56);
-  st.z = mix16(s.w64(n - 48) + len, s.w64(n - 24));
-  st.v = weak32_at(s, n - 64, len, st.z);
-  st.w = weak32_at(s, n - 32, st.y + kK1, st.x);
-  st.x = st.x * kK1 + s.w64(0);
+  {  // tail-first initialisation from the last 64 bytes (city.c:237-243)
+    const Words<16> t = s.template span<64>(n - 64);
+    const u64 x = t.w64(24);  // s+len-40
+    st.y = t.w64(48) + t.w64(8);
+    st.z = mix16(t.w64(16) + len, t.w64(40));
+    st.v = weak32_at(t, 0, len, st.z);
+    st.w = weak32_at(t, 32, st.y + kK1, x);
+    st.x = x * kK1 + fetch64(s, 0);
+  }
   const u32 rounds = (u32)((len - 1) >> 6);
-  for (u32 r = 0; r < rounds; ++r) round64(st, s, r << 6);
+  for (u32 r = 0; r < rounds; ++r) round64(st, s.template span<64>(r << 6));
   return mix16(mix16(st.v.lo, st.w.lo) + smix(st.y) * kK1 + st.z,
                mix16(st.v.hi, st.w.hi) + st.x);
 }
@@ -235,18 +283,20 @@ PDHT_HD u128 murmur128(const R &s, u64 len, u128 seed) {
   if (len <= 16) {
     a = smix(a * kK1) * kK1;
     c = b * kK1 + len0to16(s, len);
-    d = smix(a + (len >= 8 ? s.w64(0) : c));
+    d = smix(a + (len >= 8 ? fetch64(s, 0) : c));
   } else {
     const u32 n = (u32)len;
-    c = mix16(s.w64(n - 8) + kK1, a);
-    d = mix16(b + len, c + s.w64(n - 16));
+    const Words<4> t = s.template span<16>(n - 16);
+    c = mix16(t.w64(8) + kK1, a);
+    d = mix16(b + len, c + t.w64(0));
     a += d;
     const u32 steps = (n - 1) >> 4;  // signed l = len-16; do..while (l > 0)
     for (u32 k = 0; k < steps; ++k) {
-      a ^= smix(s.w64(16 * k) * kK1) * kK1;
+      const Words<4> q = s.template span<16>(16 * k);
+      a ^= smix(q.w64(0) * kK1) * kK1;
       a *= kK1;
       b ^= a;
-      c ^= smix(s.w64(16 * k + 8) * kK1) * kK1;
+      c ^= smix(q.w64(8) * kK1) * kK1;
       c *= kK1;
       d ^= c;
     }
@@ -264,15 +314,18 @@ PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
   st.x = seed.lo;
   st.y = seed.hi;
   st.z = len * kK1;
-  st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + s.w64(0);
-  st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + s.w64(8);
+  {
+    const Words<4> h = s.template span<16>(0);
+    st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + h.w64(0);
+    st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + h.w64(8);
+  }
   st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
-  st.w.hi = rotr_nz(st.x + s.w64(88), 53) * kK1;
+  st.w.hi = rotr_nz(st.x + fetch64(s, 88), 53) * kK1;
   u32 o = 0;
   u64 rem = len;
   do {
-    round64(st, s, o);
-    round64(st, s, o + 64);
+    round64(st, s.template span<64>(o));
+    round64(st, s.template span<64>(o + 64));
     o += 128;
     rem -= 128;
   } while (rem >= 128);
@@ -280,15 +333,15 @@ PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
   u128 v = st.v, w = st.w;
   x += rotr_nz(v.lo + z, 49) * kK0;
   z += rotr_nz(w.lo, 37) * kK0;
-  for (u32 done = 0; done < (u32)rem;) {  // city.c:357-365, tail from the end
+  for (u32 done = 0; done < (u32)rem;) {  // city.c:357-365, 32-B chunks from the end
     done += 32;
-    const u32 p = o + (u32)rem - done;
+    const Words<8> p = s.template span<32>(o + (u32)rem - done);
     y = rotr_nz(x + y, 42) * kK0 + v.hi;
-    w.lo += s.w64(p + 16);
+    w.lo += p.w64(16);
     x = x * kK0 + w.lo;
-    z += w.hi + s.w64(p);
+    z += w.hi + p.w64(0);
     w.hi += v.lo;
-    v = weak32_at(s, p, v.lo + z, v.hi);
+    v = weak32_at(p, 0, v.lo + z, v.hi);
   }
   x = mix16(x, v.lo);
   y = mix16(y + z, w.lo);
@@ -299,11 +352,12 @@ PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
 template <class R>
 PDHT_HD u128 city128(const R &s, u64 len) {
   if (len >= 16) {
-    return city128_seed(Shifted<R>{s, 16}, len - 16, u128{s.w64(0) ^ kK3, s.w64(8)});
+    const Words<4> h = s.template span<16>(0);
+    return city128_seed(Shifted<R>{s, 16}, len - 16, u128{h.w64(0) ^ kK3, h.w64(8)});
   }
   if (len >= 8) {
     // WithSeed(NULL, 0, seed): no key byte is read after the seed is formed
-    const u128 seed{s.w64(0) ^ (len * kK0), s.w64((u32)len - 8) ^ kK1};
+    const u128 seed{fetch64(s, 0) ^ (len * kK0), fetch64(s, (u32)len - 8) ^ kK1};
     return murmur128(s, 0, seed);
   }
   return murmur128(s, len, u128{kK0, kK1});
@@ -343,41 +397,25 @@ PDHT_HD u64 crc32c_u64(u64 crc, u64 v) {
          T.t[1][(x >> 48) & 0xff] ^ T.t[0][x >> 56];
 }
 
-// Zero-padded view used by CityHashCrc256Short (city.c:476-481): bytes past
-// `len` of the underlying key read as 0.
-template <class R>
-struct PadReader {
-  const R &r;
-  u32 len;
-  PDHT_HD u64 w64(u32 o) const {
-    if (o + 8 <= len) return r.w64(o);
-    u64 v = 0;
-    for (u32 i = 0; i < 8; ++i)
-      if (o + i < len) v |= (u64)r.b8(o + i) << (8 * i);
-    return v;
-  }
-  PDHT_HD u32 w32(u32 o) const { return (u32)w64(o); }
-  PDHT_HD u32 b8(u32 o) const { return o < len ? r.b8(o) : 0u; }
-};
-
 // city.c:407-473 (CityHashCrc256Long), len >= 240
 template <class R>
 PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4]) {
-  u64 a = s.w64(56) + kK0;
-  u64 b = s.w64(96) + kK0;
+  u64 a = fetch64(s, 56) + kK0;
+  u64 b = fetch64(s, 96) + kK0;
   u64 c = out[0] = mix16(b, len);
-  u64 d = out[1] = s.w64(120) * kK0 + len;
-  u64 e = s.w64(184) + seed;
+  u64 d = out[1] = fetch64(s, 120) * kK0 + len;
+  u64 e = fetch64(s, 184) + seed;
   u64 f = seed, g = 0, h = 0, i = 0, j = 0;
   u64 t = c + d;
   u32 o = 0;
-  auto chunk = [&](u64 mult, u32 flip) {
+  auto chunk = [&](u64 mult, u32 flip) {  // one 40-byte CHUNK (city.c:425-440)
+    const Words<10> q = s.template span<40>(o);
     const u64 a0 = a;
-    a = rotr(b, 41u ^ flip) * mult + s.w64(o);
-    b = rotr(c, 27u ^ flip) * mult + s.w64(o + 8);
-    c = rotr(d, 41u ^ flip) * mult + s.w64(o + 16);
-    d = rotr(e, 33u ^ flip) * mult + s.w64(o + 24);
-    e = rotr(t, 25u ^ flip) * mult + s.w64(o + 32);
+    a = rotr(b, 41u ^ flip) * mult + q.w64(0);
+    b = rotr(c, 27u ^ flip) * mult + q.w64(8);
+    c = rotr(d, 41u ^ flip) * mult + q.w64(16);
+    d = rotr(e, 33u ^ flip) * mult + q.w64(24);
+    e = rotr(t, 25u ^ flip) * mult + q.w64(32);
     t = a0;
     f = crc32c_u64(f, a);
     g = crc32c_u64(g, b);

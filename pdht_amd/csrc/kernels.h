@@ -28,41 +28,62 @@ constexpr int kBlock = 256;  // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 
 // --------------------------------------------------------------- readers ---
-// Key bytes in LDS at an arbitrary byte offset.  Each dword fetch reads the
-// two covering dwords and funnels them with v_alignbyte_b32; the window
-// carries 16 B of slack so the trailing dword read stays in the array.
+// Key bytes in LDS at an arbitrary byte offset.  A span of N bytes is one run
+// of N/4+1 dword reads from one base address (ds_read2_b32 with immediate
+// offsets, a single wait) funnelled by v_alignbyte_b32; the window carries
+// 16 B of slack so the trailing dword read stays in the array.
 struct LdsReader {
   const u32 *lds;
   u32 base;
-  __device__ __forceinline__ u32 dw(u32 o) const {
-    o += base;
-    const u32 q = o >> 2;
-    return __builtin_amdgcn_alignbyte(lds[q + 1], lds[q], o & 3u);
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> span(u32 o) const {
+    const u32 a = base + o;
+    const u32 *p = lds + (a >> 2);
+    const u32 r = a & 3u;
+    u32 raw[N / 4 + 1];
+#pragma unroll
+    for (int j = 0; j <= N / 4; ++j) raw[j] = p[j];
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) w.d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], r);
+    return w;
   }
-  __device__ __forceinline__ u64 w64(u32 o) const { return ((u64)dw(o + 4) << 32) | dw(o); }
-  __device__ __forceinline__ u32 w32(u32 o) const { return dw(o); }
+  __device__ __forceinline__ u32 w32(u32 o) const { return span<4>(o).d[0]; }
   __device__ __forceinline__ u32 b8(u32 o) const {
-    o += base;
-    return (lds[o >> 2] >> (8 * (o & 3u))) & 0xffu;
+    const u32 a = base + o;
+    return (lds[a >> 2] >> (8 * (a & 3u))) & 0xffu;
   }
-  __device__ __forceinline__ LdsReader at(u32 o) const { return LdsReader{lds, base + o}; }
 };
 
-// Key bytes straight from global memory (keys larger than the LDS window).
+// Key bytes straight from global memory (keys outside the LDS window): the
+// same dword-run + funnel shape on the dword-aligned address.  The extra
+// trailing dword is only read when the span is misaligned (it then holds key
+// bytes), so no read leaves the key's dwords.
+// Loads go through explicit global-address-space pointers: a generic (flat)
+// load would make the compiler drain vmcnt AND lgkmcnt at every join after
+// it, i.e. wait for the next tile's prefetch on the common path too.
+typedef const __attribute__((address_space(1))) u32 gu32;
+typedef const __attribute__((address_space(1))) uint8_t gu8;
 struct GlobalReader {
   const uint8_t *p;
-  __device__ __forceinline__ u64 w64(u32 o) const {
-    u64 v;
-    __builtin_memcpy(&v, p + o, 8);
-    return v;
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> span(u32 o) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
+    gu32 *q = reinterpret_cast<gu32 *>(a & ~(uintptr_t)3);
+    const u32 r = (u32)(a & 3);
+    u32 raw[N / 4 + 1];
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) raw[j] = q[j];
+    raw[N / 4] = r ? q[N / 4] : 0u;
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) w.d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], r);
+    return w;
   }
-  __device__ __forceinline__ u32 w32(u32 o) const {
-    u32 v;
-    __builtin_memcpy(&v, p + o, 4);
-    return v;
+  __device__ __forceinline__ u32 w32(u32 o) const { return span<4>(o).d[0]; }
+  __device__ __forceinline__ u32 b8(u32 o) const {
+    return reinterpret_cast<gu8 *>(reinterpret_cast<uintptr_t>(p))[o];
   }
-  __device__ __forceinline__ u32 b8(u32 o) const { return p[o]; }
-  __device__ __forceinline__ GlobalReader at(u32 o) const { return GlobalReader{p + o}; }
 };
 
 // ------------------------------------------------------------ algorithms ---
@@ -247,9 +268,7 @@ __device__ __forceinline__ void load_key_regs(const uint8_t *__restrict__ keys, 
       r.d[4 * j + 2] = v.z;
       r.d[4 * j + 3] = v.w;
     }
-  }
-  r.base = 0;
-}
+  }}
 
 // ------------------------------------------------------- direct kernel ---
 // U keys per lane per iteration (all loads issued before any hashing).
@@ -307,9 +326,7 @@ __device__ __forceinline__ void read_row_asm(u32 img, u32 lane, RegReader<16> &r
     r.d[4 * c + 1] = v[c].y;
     r.d[4 * c + 2] = v[c].z;
     r.d[4 * c + 3] = v[c].w;
-  }
-  r.base = 0;
-}
+  }}
 
 // Variant "lds": pieces arrive by LDS-DMA (global_load_lds_dwordx4, no VGPR
 // staging); the SOURCE address is permuted so that the linear DMA image is
@@ -346,9 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_lds64(const uint8_t *__restric
   for (; t < ntiles; t += nwaves) {
     const u64 tn = t + nwaves;
     const u64 i = (t << 6) + lane;
-    RegReader<16> r;
-    r.base = 0;
-    if (t < full) {
+    RegReader<16> r;    if (t < full) {
       if (tn < full) {
         issue(tn, b ^ 1);  // next tile streams in while this one hashes
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -393,9 +408,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restr
   for (; t < ntiles; t += nwaves) {
     const u64 tn = t + nwaves;
     const u64 i = (t << 6) + lane;
-    RegReader<16> r;
-    r.base = 0;
-    if (t < full) {
+    RegReader<16> r;    if (t < full) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const u32 g = 64 * j + lane;
@@ -427,8 +440,8 @@ __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restr
 // --------------------------------------------------------- window kernel ---
 // Any key length.  VAR: key i = bytes[offsets[i]-obase, offsets[i+1]-obase);
 // otherwise key i = bytes[i*stride, i*stride+keylen).  WIN = LDS bytes per
-// wave.
-template <int WIN, bool VAR, class Algo, class Sink>
+// wave.  AUX = cache-policy bits of the LDS-DMA (2 = non-temporal).
+template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0>
 __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -448,20 +461,27 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
     const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;  // one past the tile's last key
     const u64 i = k0 + lane;
     const bool valid = i < n;
-    u64 start = 0, end = 0, wlo, whi;
+    u64 start = 0, end = 0, whi;
     if constexpr (VAR) {
       if (valid) {
         start = offsets[i] - obase;
         end = offsets[i + 1] - obase;
       }
-      wlo = offsets[k0] - obase;
       whi = offsets[kend] - obase;
     } else {
       start = i * stride;
       end = start + keylen;
-      wlo = k0 * stride;
       whi = (kend - 1) * stride + keylen;
     }
+    // One pass: the window starts at the tile's first key; keys that end
+    // beyond WIN bytes (only in tiles of long keys) are read from global
+    // memory instead (a multi-pass variant that re-staged the remainder was
+    // measured slower: each extra pass is a serialised DMA round trip).
+    u64 wlo;
+    if constexpr (VAR)
+      wlo = offsets[k0] - obase;
+    else
+      wlo = k0 * stride;
     wlo &= ~(u64)15;
     const u64 span = whi - wlo;
     const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
@@ -474,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
         if ((u32)j * 1024 + lane * 16 < wbytes)
           __builtin_amdgcn_global_load_lds(
               (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
-              (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, 0);
+              (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, AUX);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -489,6 +509,183 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
       sink.put(i, h);
     }
     __builtin_amdgcn_wave_barrier();  // window reused by the next tile
+  }
+  sink.flush();
+}
+
+// ------------------------------------------------- pipelined window kernel ---
+// k_window with the next tile's window prefetched into VGPRs (WIN/1024
+// global_load_dwordx4 per lane, contiguous 1 KiB per wave-instruction) while
+// the current tile hashes out of LDS; the prefetched pieces are written into
+// the (single) per-wave LDS window with ds_write_b128 at the top of the next
+// iteration.  Ordinary loads, so the compiler's waits stay exact (LDS-DMA
+// would make it drain every outstanding DMA before each LDS read).
+template <int WIN, bool VAR, class Algo, class Sink>
+__global__ __launch_bounds__(kBlock) void k_window_pf(const uint8_t *__restrict__ bytes,
+                                                      const u64 *__restrict__ offsets, u64 obase,
+                                                      u64 stride, u64 keylen, u64 n, Algo algo,
+                                                      Sink sink) {
+  static_assert(WIN % 1024 == 0, "window = whole 1 KiB pieces");
+  constexpr int P = WIN / 1024;
+  __shared__ __attribute__((aligned(16))) u32 win[kWavesPerBlock][WIN / 4 + 4];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *lds = win[wave];
+  u32x4 *lds4 = reinterpret_cast<u32x4 *>(lds);
+
+  struct Tile {
+    u64 wlo;      // 16-B aligned window start (byte offset into `bytes`)
+    u32 wbytes;   // bytes of the window actually staged (<= WIN)
+    u64 start, end;
+  };
+  auto geometry = [&](u64 t) {
+    Tile g;
+    const u64 k0 = t << 6;
+    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
+    const u64 i = k0 + lane;
+    u64 whi;
+    if constexpr (VAR) {
+      g.wlo = (offsets[k0] - obase) & ~(u64)15;
+      whi = offsets[kend] - obase;
+      g.start = i < n ? offsets[i] - obase : 0;
+      g.end = i < n ? offsets[i + 1] - obase : 0;
+    } else {
+      g.wlo = (k0 * stride) & ~(u64)15;
+      whi = (kend - 1) * stride + keylen;
+      g.start = i * stride;
+      g.end = g.start + keylen;
+    }
+    const u64 span = whi - g.wlo;
+    g.wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    return g;
+  };
+  u32x4 pre[P];
+  auto prefetch = [&](const Tile &g) {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(bytes + g.wlo) + lane;
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if ((u32)j * 1024 + lane * 16 < g.wbytes) pre[j] = __builtin_nontemporal_load(src + 64 * j);
+  };
+
+  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
+  Tile cur{};
+  if (t < ntiles) {
+    cur = geometry(t);
+    prefetch(cur);
+  }
+  for (; t < ntiles; t += nwaves) {
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if ((u32)j * 1024 + lane * 16 < cur.wbytes) lds4[64 * j + lane] = pre[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const Tile g = cur;
+    const u64 tn = t + nwaves;
+    if (tn < ntiles) {  // next tile streams in while this one hashes
+      cur = geometry(tn);
+      prefetch(cur);
+    }
+    const u64 i = (t << 6) + lane;
+    if (i < n) {
+      const u64 len = g.end - g.start;
+      typename Algo::Out h;
+      if (g.end - g.wlo <= g.wbytes)
+        h = algo(LdsReader{lds, (u32)(g.start - g.wlo)}, len);
+      else
+        h = algo(GlobalReader{bytes + g.start}, len);
+      sink.put(i, h);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the window is rewritten by the next tile
+  }
+  sink.flush();
+}
+
+// ------------------------------------------------ class-sorted var keys ---
+// Cost class of a key: which code path CityHash takes (city.c:225-233) and,
+// for long keys, how many 64-byte rounds (city.c:246).
+__device__ __forceinline__ u32 len_class(u64 len) {
+  if (len <= 16) return 0;
+  if (len <= 32) return 1;
+  if (len <= 64) return 2;
+  const u64 r = (len - 1) >> 6;  // 1.. rounds
+  return r >= 4 ? 6u : (u32)(2 + r);
+}
+
+// Variable-length keys, block tiles of 256 keys.  The tile's contiguous byte
+// range is DMA'd into one LDS window shared by the block; the tile's keys are
+// counting-sorted by cost class in LDS and thread t hashes the t-th key of
+// that order, so a wave runs (mostly) one code path with one trip count
+// instead of every path its 64 lanes' lengths touch.  Digests go back to
+// their original index.  Keys not inside the window (tile bytes > WINB) are
+// read from global memory.
+template <int WINB, class Algo, class Sink>
+__global__ __launch_bounds__(kBlock) void k_var_sorted(const uint8_t *__restrict__ bytes,
+                                                       const u64 *__restrict__ offsets, u64 obase,
+                                                       u64 n, Algo algo, Sink sink) {
+  static_assert(WINB % 1024 == 0, "window = whole 1 KiB DMA pieces");
+  __shared__ __attribute__((aligned(16))) u32 win[WINB / 4 + 4];
+  __shared__ u32 s_rel[kBlock], s_len[kBlock], s_perm[kBlock], s_cnt[8];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  sink.init();
+  const u32 tid = threadIdx.x;
+  const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u32 lane = tid & 63;
+  const u64 ntiles = (n + kBlock - 1) / kBlock;
+  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const u64 k0 = t * kBlock;
+    const u64 kend = (k0 + kBlock < n) ? k0 + kBlock : n;
+    const u64 i = k0 + tid;
+    const bool valid = i < n;
+    const u64 wlo = (offsets[k0] - obase) & ~(u64)15;
+    const u64 whi = offsets[kend] - obase;
+    const u64 span = whi - wlo;
+    const u32 wbytes = span < (u64)WINB ? (u32)span : (u32)WINB;
+    // DMA the window: pieces of 1 KiB, wave w takes pieces w, w+4, ...
+    const uint8_t *src = bytes + wlo;
+    for (u32 j = wave; j * 1024 < wbytes; j += kWavesPerBlock) {
+      if (j * 1024 + lane * 16 < wbytes)
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+            (void __attribute__((address_space(3))) *)(win + 256 * j), 16, 0, 0);
+    }
+    // key geometry + class while the DMA is in flight
+    u32 cls = 7;
+    if (valid) {
+      const u64 st = offsets[i] - obase, en = offsets[i + 1] - obase;
+      s_rel[tid] = (u32)(st - wlo);
+      s_len[tid] = (u32)(en - st);
+      cls = len_class(en - st);
+    }
+    if (tid < 8) s_cnt[tid] = 0;
+    __syncthreads();
+    const u32 pos = atomicAdd(&s_cnt[cls], 1u);
+    __syncthreads();
+    u32 base = 0;
+#pragma unroll
+    for (u32 c = 0; c < 7; ++c) base += (c < cls) ? s_cnt[c] : 0u;
+    s_perm[base + pos] = tid;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < kend - k0) {
+      const u32 me = s_perm[tid];
+      const u32 rel = s_rel[me], len = s_len[me];
+      typename Algo::Out h;
+      if (span <= 0xffffffffull && (u64)rel + len <= wbytes) {
+        h = algo(LdsReader{win, rel}, (u64)len);
+      } else {  // outside the window: straight from global memory
+        h = algo(GlobalReader{bytes + (offsets[k0 + me] - obase)}, (u64)len);
+      }
+      sink.put(k0 + me, h);
+    }
+    __syncthreads();  // window, perm and geometry are rewritten by the next tile
   }
   sink.flush();
 }

@@ -83,7 +83,8 @@ static FastMod make_fastmod(u64 d) {
 }
 
 // --------------------------------------------------------- launchers ---
-constexpr int kWinBytes = 12288;  // LDS window per wave (12 KiB)
+constexpr int kWinBytes = 12288;     // k_window: LDS window per wave (12 KiB)
+constexpr int kVarWinBytes = 36864;  // k_var_sorted: per 256-key tile; 4 blocks per CU
 
 // Fixed-length keys: dispatch to the register-direct / LDS-transposed kernel
 // when the length is one of the specialised ones and the layout allows it,
@@ -154,10 +155,21 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
     g_kernel = "k_fixed_direct<8,4>";
     k_fixed_direct<8, 4, Algo, Sink><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
   } else {
-    g_kernel = "k_window<fixed>";
     const u64 tiles = (n + 63) / 64;
-    k_window<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
-        k, nullptr, 0, stride, keylen, n, algo, sink);
+    if (variant == 3) {
+      g_kernel = "k_window<fixed>";
+      k_window<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink);
+    } else if (variant == 14) {
+      g_kernel = "k_window_pf<fixed>";
+      k_window_pf<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink);
+    } else {
+      typedef typename NtSink<Sink>::type SinkNt;
+      g_kernel = "k_window<fixed,nt>";
+      k_window<kWinBytes, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+    }
   }
   HIP_TRY(hipGetLastError());
   return 0;
@@ -170,10 +182,44 @@ static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n
   if (!bytes || !offsets) return fail("null bytes/offsets pointer%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
-  g_kernel = "k_window<var>";
-  const u64 tiles = (n + 63) / 64;
-  k_window<kWinBytes, true, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
-      static_cast<const uint8_t *>(bytes), offsets, obase, 0, 0, n, algo, sink);
+  const uint8_t *b = static_cast<const uint8_t *>(bytes);
+  const int variant = g_variant.load(std::memory_order_relaxed);
+  if (variant == 10) {  // class-sorted block tiles (measured slower, kept for A/B)
+    g_kernel = "k_var_sorted";
+    k_var_sorted<kVarWinBytes, Algo, Sink><<<grid_for((n + kBlock - 1) / kBlock, 4, dev), kBlock, 0, st>>>(
+        b, offsets, obase, n, algo, sink);
+  } else {
+    typedef typename NtSink<Sink>::type SinkNt;
+    const SinkNt sink_nt = NtSink<Sink>::make(sink);
+    const u64 wb = ((n + 63) / 64 + 3) / 4;  // blocks of 4 wave-tiles
+    switch (variant) {
+      case 3:
+        g_kernel = "k_window<var>";
+        k_window<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, sink);
+        break;
+      case 12:
+        g_kernel = "k_window<var,nt,8K>";
+        k_window<8192, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, sink_nt);
+        break;
+      case 13:
+        g_kernel = "k_window<var,nt,16K>";
+        k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, sink_nt);
+        break;
+      case 14:
+        g_kernel = "k_window_pf<var>";
+        k_window_pf<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, sink);
+        break;
+      default:  // 0, 11: non-temporal window DMA + digest stores (tools/varbench.py)
+        g_kernel = "k_window<var,nt>";
+        k_window<kWinBytes, true, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, sink_nt);
+        break;
+    }
+  }
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -65,7 +65,16 @@ def test_city64_every_length(dev, oracle, L):
     if L in (8, 16, 32, 64):
         assert P.last_kernel().startswith("k_fixed_"), P.last_kernel()
     else:
-        assert P.last_kernel() == "k_window<fixed>"
+        assert P.last_kernel() == "k_window<fixed,nt>"
+    if L in (13, 100, 1000):  # the other generic-length kernels too
+        for v, name in ((3, "k_window<fixed>"), (14, "k_window_pf<fixed>")):
+            old = P.set_variant(v)
+            try:
+                got = u64(P.city64_batch(to_dev(k, dev)))
+                assert P.last_kernel() == name
+            finally:
+                P.set_variant(old)
+            assert (got == oracle.city64_fixed(k)).all()
 
 
 @pytest.mark.parametrize("L", [0, 1, 3, 8, 13, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 144, 200, 901, 2000])
@@ -137,7 +146,7 @@ def test_edge_layouts(dev, oracle):
     big = rng.integers(0, 256, (1000, 80), dtype=np.uint8)
     bd = to_dev(big, dev)
     got = u64(P.city64_batch(bd[:, :64]))
-    assert P.last_kernel() == "k_window<fixed>"
+    assert P.last_kernel() == "k_window<fixed,nt>"
     assert (got == oracle.city64_fixed(big[:, :64])).all()
     flat = to_dev(rng.integers(0, 256, 64 * 777 + 1, dtype=np.uint8), dev)
     mis = flat[1:].view(777, 64)
@@ -175,7 +184,22 @@ def test_var_golden_mixed(dev, golden, oracle):
     assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
 
 
-def test_var_edge_cases(dev, oracle):
+VAR_KERNELS = {0: "k_window<var,nt>", 3: "k_window<var>", 10: "k_var_sorted",
+               11: "k_window<var,nt>", 12: "k_window<var,nt,8K>", 13: "k_window<var,nt,16K>",
+               14: "k_window_pf<var>"}
+
+
+@pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
+def test_var_edge_cases(dev, oracle, variant):
+    old = P.set_variant(variant)
+    try:
+        _var_edge_cases(dev, oracle)
+        assert P.last_kernel() == VAR_KERNELS[variant]
+    finally:
+        P.set_variant(old)
+
+
+def _var_edge_cases(dev, oracle):
     rng = np.random.default_rng(9)
     # empty keys, 1..3-byte keys, keys far longer than the LDS window, all mixed
     lens = np.concatenate([np.zeros(40, np.int64), rng.integers(0, 40, 300),

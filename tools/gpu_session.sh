@@ -25,6 +25,14 @@ for step in "$@"; do
              for ctr in FETCH_SIZE WRITE_SIZE; do
                timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$ctr" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/pmc_$ctr.log 2>&1 || { rc=$?; break; }
              done ;;
+    vartests) timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider -k "var or cfg3 or host or smoke" > gpurun_out/gpu_vartests.log 2>&1; rc=$?
+             tail -3 gpurun_out/gpu_vartests.log ;;
+    varbench) timeout -k 10 300 python tools/varbench.py --variants ${VARIANTS:-0,11,12,13,14,10} > gpurun_out/varbench.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/varbench.log ;;
+    counters) timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; rc=$?; rc=0 ;;
+    sq_*)    cfg=${step#sq_}
+             timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sq_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/sq_$cfg.log 2>&1; rc=$?
+             tail -3 gpurun_out/sq_$cfg.log | cut -c1-300 ;;
     *) echo "unknown step $step"; rc=0 ;;
   esac
   echo "[step $step rc=$rc]"

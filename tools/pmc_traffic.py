@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, as
+MI355X_MICROARCH.md §rocprofv3 requires) into HBM bytes per hash-kernel launch.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts exactly half
+the bytes of a wide coalesced streaming read (16 B per lane, global_load and
+LDS-DMA alike) -> x2.  WRITE_SIZE is exact for streaming stores.  Both are in
+KiB.
+
+  python tools/pmc_traffic.py --cfg cfg2 --keys 16777216 --kernel k_fixed_xpose64 \
+      --dir gpurun_out --out profiles/traffic_cfg2.json
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+
+def per_launch(path, kernel, counter):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kernel} in {path}")
+    return statistics.median(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", required=True)
+    ap.add_argument("--keys", type=int, required=True)
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--algo-bytes-per-key", type=float, required=True)
+    ap.add_argument("--dir", default="gpurun_out")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    f_kib, nf = per_launch(os.path.join(a.dir, "pmc_FETCH_SIZE", "run_counter_collection.csv"),
+                           a.kernel, "FETCH_SIZE")
+    w_kib, nw = per_launch(os.path.join(a.dir, "pmc_WRITE_SIZE", "run_counter_collection.csv"),
+                           a.kernel, "WRITE_SIZE")
+    fetch = f_kib * 1024 * 2  # gfx950: FETCH_SIZE = half of a wide streaming read
+    write = w_kib * 1024
+    algo = a.algo_bytes_per_key * a.keys
+    res = {"cfg": a.cfg, "kernel": a.kernel, "keys_per_launch": a.keys,
+           "fetch_size_kib_raw": f_kib, "fetch_correction": 2, "write_size_kib_raw": w_kib,
+           "launches_sampled": [nf, nw],
+           "hbm_bytes_per_launch": int(fetch + write),
+           "algorithmic_bytes_per_launch": int(algo),
+           "traffic_over_algorithmic": round((fetch + write) / algo, 4)}
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
