@@ -1,26 +1,31 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident batch CityHash64 on 64-byte keys (BASELINE.json).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|place]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5|place]
 
 One step = one pass of the hot path (one kernel launch) over this GPU's batch
 of synthetic keys already resident in HBM.  Default workload = BASELINE
 configs[1] ("cfg2": 16M x 64 B keys per GPU, CityHash64).  For N > 1 (launched
-by torch.distributed.run) each rank hashes its own contiguous shard of the
-same key stream (keys [r*n, (r+1)*n)): independent slices, no collective on
-the data path (weak scaling); the only collectives are the timing barrier and
-the max-over-ranks of the elapsed time.
+by torch.distributed.run, one rank per GPU) rank r hashes its own contiguous
+slice [r*n, (r+1)*n) of the same key stream (pdht_amd.dist.weak_shard): no
+collective on the data path (weak scaling); the only collectives are the
+timing barrier, the max of elapsed times and the parity reductions.
+"cfg5" = 128M keys per GPU, i.e. BASELINE configs[4] (1B keys) at N = 8.
 
 Rank 0 prints one JSON line.  Besides the contract fields it carries
   roofline      -- achieved algorithmic HBM GB/s of the hash kernel (72 B/key:
                    64 B key read + 8 B digest write) over its average launch
-                   duration measured with HIP events on the launch stream;
+                   duration measured with HIP events on the launch stream,
+                   plus HBM traffic per launch from the committed rocprofv3
+                   PMC pass (profiles/traffic_<cfg>.json) and a calibrated
+                   read-stream rate on the same buffer;
   cpu_baseline  -- the reference city.c (oracle/_ref, or the oracle port when
                    _ref is absent) timed on this host's cores over a bounded
                    sample of the same keys (rank 0, N = 1 only);
   host_resident -- the same hash with keys/digests in pinned host memory
                    (H2D + kernel + D2H pipeline), N = 1 only;
-  parity        -- digests checked against the oracle / reference golden folds.
+  parity        -- this run's digests checked against the oracle (sample)
+                   and against the reference golden fold of every shard.
 """
 from __future__ import annotations
 
@@ -47,13 +52,21 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "place"])
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "place"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
-    ap.add_argument("--variant", type=int, default=0, help="64-B kernel: 0 auto, 1 direct, 2 lds, 3 window")
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant (tools/kbench.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline")
     return ap.parse_args()
+
+
+def golden_folds():
+    p = os.path.join(ROOT, "tests", "golden", "config_folds.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)["configs"]
 
 
 def main():
@@ -61,9 +74,9 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from pdht_amd import dist as D
+
+    rank, local, world = D.env_rank_world()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -80,34 +93,37 @@ def main():
 
     cfg = a.config
     # ---------------------------------------------------------- workload ---
-    if cfg in ("cfg2", "cfg4", "place"):
-        L = 64 if cfg != "place" else 8
-        n = a.keys_per_gpu or 16 * M
-        first = rank * n
-        words = P.splitmix64_fill(SEED_KEYS, first * L // 8, n * L // 8, device=dev)
+    keys = out = data = offs = None
+    if cfg in ("cfg2", "cfg4", "cfg5", "place"):
+        L = 8 if cfg == "place" else 64
+        n = a.keys_per_gpu or (128 * M if cfg == "cfg5" else 16 * M)
+        sh = D.weak_shard(rank, world, n)
+        words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
-        dbytes = 16 if cfg == "cfg4" else 8
-        if cfg == "cfg2":
+        if cfg in ("cfg2", "cfg5"):
             out = torch.empty(n, dtype=torch.int64, device=dev)
             step = lambda: P.city64_batch(keys, out=out)  # noqa: E731
             bytes_per_key = 64 + 8
-            workload = "cfg2: CityHash64 over 16M x 64B keys per GPU, device-resident"
+            workload = (f"{cfg}: CityHash64 over {n >> 20}M x 64B keys per GPU, device-resident"
+                        + (" (BASELINE configs[4] = 1B keys at N=8)" if cfg == "cfg5" else ""))
         elif cfg == "cfg4":
             out = torch.empty((n, 2), dtype=torch.int64, device=dev)
             step = lambda: P.citycrc128_batch(keys, out=out)  # noqa: E731
             bytes_per_key = 64 + 16
-            workload = "cfg4: CityHashCrc128 over 16M x 64B keys per GPU, device-resident"
+            workload = f"cfg4: CityHashCrc128 over {n >> 20}M x 64B keys per GPU, device-resident"
         else:
             hist = torch.zeros(1024, dtype=torch.int64, device=dev)
-            out = None
-            step = lambda: P.place_batch(keys, 1, 1024, ptindex=True, rank=True, hist=hist)  # noqa: E731
+            outs = P.place_batch(keys, 3, 1024, hist=hist)
+            out = outs[0]
+            step = lambda: P.place_batch(keys, 3, 1024, hist=hist, out=outs)  # noqa: E731
             bytes_per_key = 8 + 8 + 4 + 4
-            workload = "place: fused pdht_hash (mbits+ptindex+rank+hist) over 16M x 8B keys per GPU"
+            workload = f"place: fused pdht_hash (mbits+ptindex+rank+hist) over {n >> 20}M x 8B keys per GPU"
         total_bytes_in = n * L
     else:  # cfg3 mixed lengths
+        L = None
         n = a.keys_per_gpu or 64 * M
-        first = rank * n
-        lens = P.mixed_lengths(SEED_LENS, first, n, 16, 256, device=dev)
+        sh = D.weak_shard(rank, world, n)
+        lens = P.mixed_lengths(SEED_LENS, sh.first, n, 16, 256, device=dev)
         offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         torch.cumsum(lens, 0, out=offs[1:])
         total = int(offs[-1].item())
@@ -115,48 +131,37 @@ def main():
         # rank 0 hashes the canonical cfg3 byte stream (golden-checked); rank r
         # takes a disjoint segment of the same splitmix64 stream
         words = P.splitmix64_fill(SEED_KEYS, rank << 40, (total + 7) // 8 + 2, device=dev)
-        data = words.view(torch.uint8)
+        data = words.view(torch.uint8)[:total]
         out = torch.empty(n, dtype=torch.int64, device=dev)
-        step = lambda: P.city64_var_batch(data[:total], offs, out=out)  # noqa: E731
+        step = lambda: P.city64_var_batch(data, offs, out=out)  # noqa: E731
         bytes_per_key = total / n + 8 + 8
         total_bytes_in = total
-        L = None
-        workload = "cfg3: CityHash64 over 64M mixed 16..256B keys per GPU (offset-indexed)"
+        workload = f"cfg3: CityHash64 over {n >> 20}M mixed 16..256B keys per GPU (offset-indexed)"
     torch.cuda.synchronize()
 
     # ------------------------------------------------------------ timing ---
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
     for _ in range(a.warmup):
         step()
     kernel_name = P.last_kernel()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(a.steps)]
-    barrier()
+    D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:
+    for s, e in ev:  # events on the stream the kernels are launched on
         s.record()
         step()
         e.record()
     torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    D.barrier()
+    elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
+    elapsed, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=dev)
 
     # -------------------------------------------- achievable read stream ---
     calib = None
-    if cfg in ("cfg2", "cfg4"):
+    if keys is not None:
         P.read_stream(keys, True)
         cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(10)]
@@ -166,22 +171,16 @@ def main():
             e.record()
         torch.cuda.synchronize()
         cms = float(np.median([s.elapsed_time(e) for s, e in cev]))
-        calib = round(n * L / (cms / 1e3) / 1e9, 1)
+        calib = round(keys.numel() / (cms / 1e3) / 1e9, 1)
 
     # ------------------------------------------------------------ parity ---
-    parity = check_parity(P, torch, cfg, rank, world, n, first, out, locals())
-    if world > 1:
-        ok = torch.tensor([1 if parity.startswith("ok") else 0], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if not int(ok.item()):
-            parity = "FAILED on some rank: " + parity
+    parity = check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev)
 
     # ------------------------------------------------------- report ------
-    total_keys = n * world * a.steps
-    value = total_keys / elapsed / 1e9
+    value = n * world * a.steps / elapsed / 1e9
     achieved = bytes_per_key * n / (kern_ms / 1e3) / 1e9
     res = {
-        "metric": METRIC if cfg == "cfg2" else f"{cfg}: Gkeys/s and achieved HBM GB/s",
+        "metric": METRIC if cfg in ("cfg2", "cfg5") else f"{cfg}: Gkeys/s and achieved HBM GB/s",
         "value": round(value, 4),
         "unit": "Gkeys/s",
         "n_gpus": world,
@@ -195,7 +194,7 @@ def main():
         "data": "synthetic: splitmix64 key bytes (seed 0x5EED5EED5EED5EED), generated on device",
         "config": {"workload": workload, "keys_per_gpu": n, "key_bytes": L,
                    "bytes_per_key": round(bytes_per_key, 3), "kernel": kernel_name,
-                   "parallelism": f"{world} independent shards, no collective"},
+                   "parallelism": f"{world} independent shards, no collective on the data path"},
         "hbm_GBps": round(achieved * world, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
@@ -207,7 +206,7 @@ def main():
     }
     if rank == 0 and world == 1 and cfg in ("cfg2", "cfg4") and not a.no_host:
         res["host_resident"] = host_rate(P, torch, n, cfg)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and cfg in ("cfg2",):
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and cfg == "cfg2":
         res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -230,48 +229,63 @@ def load_traffic(cfg, n):
         return None
 
 
-def check_parity(P, torch, cfg, rank, world, n, first, out, env):
-    """Bit-exact check of this rank's digests against the oracle on a sample and,
-    where the shard matches a golden config, the full fold checksum."""
+def golden_shard_fold(folds, cfg, sh):
+    """Reference fold of exactly this shard's keys, when the golden file has it."""
+    if folds is None:
+        return None, None
+    if cfg in ("cfg2", "cfg5"):
+        c5 = folds.get("cfg5_city64_1B_x64", {})
+        if sh.n == 16 * M and sh.first % (16 * M) == 0 and "chunks" in c5:
+            j = sh.first // (16 * M)
+            if j < len(c5["chunks"]):
+                return int(c5["chunks"][j], 16), f"cfg5 chunk {j} (keys {sh.first}..+16M)"
+        if sh.n == 128 * M and sh.first % (128 * M) == 0:
+            j = sh.first // (128 * M)
+            if j < 8:
+                return int(c5["shards"][j], 16), f"cfg5 shard {j}"
+        if sh.first == 0 and sh.n == 16 * M:
+            return int(folds["cfg2_city64_16M_x64"]["total"], 16), "cfg2 total"
+    if cfg == "cfg4" and sh.first == 0 and sh.n == 16 * M:
+        return int(folds["cfg4_crc128_16M_x64"]["total"], 16), "cfg4 total"
+    if cfg == "cfg3" and sh.rank == 0 and sh.n == 64 * M:
+        return int(folds["cfg3_city64_64M_mixed"]["total"], 16), "cfg3 total"
+    return None, None
+
+
+def check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev):
+    """Bit-exact check of this rank's digests: a sample against the oracle
+    and the whole shard's fold against the reference golden fold."""
     try:
         from oracle import oracle as O
     except Exception as e:  # pragma: no cover
         return f"unchecked (oracle unavailable: {e})"
     msgs = []
-    if cfg in ("cfg2", "cfg4", "place"):
-        L = 64 if cfg != "place" else 8
-        s = min(n, 65536)
-        k = O.fixed_keys(s, L, first_key=first)
-        got = out[:s].cpu().numpy().view(np.uint64) if cfg != "place" else None
-        if cfg == "cfg2":
-            ok = (got == O.city64_fixed(k)).all()
-        elif cfg == "cfg4":
+    s = min(sh.n, 65536)
+    if cfg in ("cfg2", "cfg4", "cfg5", "place"):
+        L = 8 if cfg == "place" else 64
+        k = O.fixed_keys(s, L, first_key=sh.first)
+        got = out[:s].cpu().numpy().view(np.uint64)
+        if cfg == "cfg4":
             ok = (got.reshape(-1, 2) == O.city128_fixed(k, crc=True)).all()
+        elif cfg == "place":
+            ok = (got == O.pdht_hash_fixed(k, 3, 1024)[0]).all()
         else:
-            mb, _, _ = P.place_batch(env["keys"][:s], 1, 1024)
-            ok = (mb.cpu().numpy().view(np.uint64) == O.pdht_hash_fixed(k, 1, 1024)[0]).all()
-        msgs.append(f"{s} keys vs oracle {'ok' if ok else 'MISMATCH'}")
-        if not ok:
-            return "FAILED: " + "; ".join(msgs)
-        gf = os.path.join(ROOT, "tests", "golden", "config_folds.json")
-        if cfg in ("cfg2", "cfg4") and first == 0 and n == 16 * M and os.path.exists(gf):
-            with open(gf) as f:
-                folds = json.load(f)["configs"]
-            key = "cfg2_city64_16M_x64" if cfg == "cfg2" else "cfg4_crc128_16M_x64"
-            d = out.reshape(-1)
-            idx = torch.arange(d.numel(), device=d.device, dtype=torch.int64)
-            fold = int((d * (2 * idx + 1)).sum().item()) & 0xFFFFFFFFFFFFFFFF
-            if f"{fold:016x}" != folds[key]["total"]:
-                return "FAILED: full fold mismatch vs reference golden " + key
-            msgs.append(f"full {n}-key fold == reference golden ({key})")
+            ok = (got == O.city64_fixed(k)).all()
     else:
-        offs = env["offs"][: 65537].cpu().numpy().astype(np.uint64)
-        data = env["data"][: int(offs[-1])].cpu().numpy()
-        ok = (out[:65536].cpu().numpy().view(np.uint64) == O.city64_var(data, offs)).all()
-        msgs.append(f"65536 mixed keys vs oracle {'ok' if ok else 'MISMATCH'}")
-        if not ok:
-            return "FAILED: " + "; ".join(msgs)
-    return "ok: " + "; ".join(msgs)
+        o = offs[: s + 1].cpu().numpy().astype(np.uint64)
+        d = data[: int(o[-1])].cpu().numpy()
+        ok = (out[:s].cpu().numpy().view(np.uint64) == O.city64_var(d, o)).all()
+    msgs.append(f"{s} keys vs oracle {'ok' if ok else 'MISMATCH'}")
+    want, what = golden_shard_fold(golden_folds(), cfg, sh)
+    fold_ok = True
+    if want is not None:
+        first_idx = 2 * sh.first if cfg == "cfg4" else sh.first
+        fold_ok = D.fold_tensor(out, first_idx) == want
+        msgs.append(f"full-shard fold {'==' if fold_ok else '!='} reference golden ({what})")
+    all_ok = D.allreduce_min_flag(bool(ok) and fold_ok, device=dev)
+    if sh.world > 1:
+        msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
+    return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
 
 
 def host_rate(P, torch, n, cfg):

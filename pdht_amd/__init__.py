@@ -335,19 +335,23 @@ def citycrc128_var_batch(data, offsets, out=None, stream=None):
 
 
 def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=None,
-                stream=None):
+                stream=None, out=None):
     """Fused pdht_hash (hash.c:25-30) over keys [n, keysize] (packed, CUDA).
 
     Returns (mbits int64[n], ptindex int32[n] | None, rank int32[n] | None);
     if `hist` (int64[nranks], CUDA) is given, per-rank counts are added to it.
+    `out` = a previous return value to reuse its tensors.
     """
     torch = _torch()
     n, L, stride = _keys_2d(keys)
     if stride != L:
         raise ValueError("place_batch needs packed keys")
-    mb = torch.empty(n, dtype=torch.int64, device=keys.device)
-    pt = torch.empty(n, dtype=torch.int32, device=keys.device) if ptindex else None
-    rk = torch.empty(n, dtype=torch.int32, device=keys.device) if rank else None
+    if out is not None:
+        mb, pt, rk = out
+    else:
+        mb = torch.empty(n, dtype=torch.int64, device=keys.device)
+        pt = torch.empty(n, dtype=torch.int32, device=keys.device) if ptindex else None
+        rk = torch.empty(n, dtype=torch.int32, device=keys.device) if rank else None
     _check(lib().pdht_place_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(mb),
                                       _dptr(pt) if pt is not None else None,
                                       _dptr(rk) if rk is not None else None, 4,

@@ -1,0 +1,95 @@
+"""Multi-GPU orchestration of the batch hash: independent shards, no
+collective on the data path.
+
+A key batch is split by key index into contiguous per-rank slices; each rank
+hashes its slice on its own GPU.  The only collectives are the ones a
+benchmark or a caller needs around the data path: a start barrier, the max
+of per-rank elapsed times, and (for verification) the sum of per-rank fold
+checksums, which equals the fold of the whole batch because the fold is
+position-weighted by GLOBAL key index (sum_i d_i * (2i+1) mod 2^64).
+
+Backend-agnostic: "nccl" (RCCL on ROCm) on GPUs, "gloo" in the CPU tests.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+MASK64 = (1 << 64) - 1
+
+
+@dataclass(frozen=True)
+class Shard:
+    rank: int
+    world: int
+    first: int  # global index of this rank's first key
+    n: int      # keys on this rank
+
+
+def env_rank_world() -> tuple[int, int, int]:
+    """(rank, local_rank, world) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def weak_shard(rank: int, world: int, n_per_rank: int) -> Shard:
+    """Weak scaling: every rank gets n_per_rank keys, rank r the slice
+    [r*n, (r+1)*n) of the global key stream."""
+    return Shard(rank, world, rank * n_per_rank, n_per_rank)
+
+
+def strong_shard(rank: int, world: int, n_total: int) -> Shard:
+    """Strong scaling: n_total keys split as evenly as possible, contiguous."""
+    lo = n_total * rank // world
+    hi = n_total * (rank + 1) // world
+    return Shard(rank, world, lo, hi - lo)
+
+
+def fold_tensor(d, first_index: int) -> int:
+    """Position-weighted fold of a digest tensor (int64 view of u64 digests,
+    flattened; 128-bit digests contribute 2 entries per key and the caller
+    passes first_index = 2*first_key)."""
+    import torch
+    d = d.reshape(-1)
+    idx = torch.arange(d.numel(), device=d.device, dtype=torch.int64) + first_index
+    return int((d * (2 * idx + 1)).sum().item()) & MASK64
+
+
+def _to_signed(v: int) -> int:
+    v &= MASK64
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def allreduce_fold(local_fold: int, device=None) -> int:
+    """Sum of per-rank folds mod 2^64 (int64 two's-complement wraparound)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([_to_signed(local_fold)], dtype=torch.int64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item()) & MASK64
+
+
+def allreduce_max(values, device=None) -> list[float]:
+    """Element-wise max over ranks (the bench's elapsed / kernel times)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def allreduce_min_flag(ok: bool, device=None) -> bool:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def barrier():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()

@@ -135,6 +135,7 @@ def folds_full(R) -> dict:
         per = n // shards
         parts = []
         chunk = 16 * M
+        chunks = []  # fold of every 16M-key chunk (weak-scaling shards of bench.py)
         for s in range(shards):
             acc = 0
             for k0 in range(s * per, (s + 1) * per, chunk):
@@ -143,14 +144,19 @@ def folds_full(R) -> dict:
                 if is128:
                     d = O.apply_ref128(keys, cnt, L=L, threads=thr, fn_name=fn)
                     # fold over the interleaved {lo,hi} array, index 2i and 2i+1
-                    acc = (acc + O.fold64(d.reshape(-1), 2 * k0)) % (1 << 64)
+                    f = O.fold64(d.reshape(-1), 2 * k0)
                 else:
                     d = O.apply_ref64(keys, cnt, L=L, threads=thr, fn_name=fn)
-                    acc = (acc + O.fold64(d, k0)) % (1 << 64)
+                    f = O.fold64(d, k0)
+                chunks.append(f)
+                acc = (acc + f) % (1 << 64)
             parts.append(acc)
             print(f"  {name} shard {s}: {acc:016x}", flush=True)
         res[name] = {"n": n, "L": L, "shards": [f"{p:016x}" for p in parts],
                      "total": f"{sum(parts) % (1 << 64):016x}"}
+        if n > chunk:
+            res[name]["chunk_keys"] = chunk
+            res[name]["chunks"] = [f"{c:016x}" for c in chunks]
 
     fixed_fold(1 * M, 64, "CityHash64", "cfg1_city64_1M_x64", shards=1)
     fixed_fold(16 * M, 64, "CityHash64", "cfg2_city64_16M_x64")

@@ -1,0 +1,93 @@
+"""The N > 1 path on CPU: world_size-2 gloo processes run bench.py's sharding
+and reductions (pdht_amd.dist) over a small key stream.
+
+Each rank hashes its weak-scaling shard with the product's scalar CityHash64
+(the same city_core.h code the kernels run), folds it by global key index and
+all-reduces: the sum of the rank folds must equal the oracle's fold of the
+whole stream, and each rank's fold must equal the oracle's fold of its slice
+-- the property bench.py relies on to check every GPU's shard independently.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+N_PER = 3000
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pdht_amd as P
+        from pdht_amd import dist as D
+        from oracle import oracle as O
+        r, lr, w = D.env_rank_world()
+        sh = D.weak_shard(r, w, N_PER)
+        keys = O.fixed_keys(sh.n, 64, first_key=sh.first)
+        d = np.array([P.CityHash64(k.tobytes()) for k in keys], dtype=np.uint64)
+        t = torch.from_numpy(d.view(np.int64))
+        local = D.fold_tensor(t, sh.first)
+        total = D.allreduce_fold(local)
+        mx = D.allreduce_max([float(r + 1), 0.5 * r])
+        ok_all = D.allreduce_min_flag(r != 1)  # rank 1 reports failure
+        D.barrier()
+        q.put({"rank": r, "first": sh.first, "n": sh.n, "local": local, "total": total,
+               "max": mx, "ok_all": ok_all,
+               "oracle_local": O.fold64(O.city64_fixed(keys), sh.first)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_helpers_single_process():
+    from pdht_amd import dist as D
+    assert D.weak_shard(3, 8, 100) == D.Shard(3, 8, 300, 100)
+    cover = [D.strong_shard(r, 3, 10) for r in range(3)]
+    assert [c.first for c in cover] == [0, 3, 6] and sum(c.n for c in cover) == 10
+    # no process group: reductions are identities
+    assert D.allreduce_max([1.5, 2.0]) == [1.5, 2.0]
+    assert D.allreduce_fold(5) == 5
+    t = torch.tensor([1, 2, 3], dtype=torch.int64)
+    assert D.fold_tensor(t, 10) == 1 * 21 + 2 * 23 + 3 * 25
+    big = torch.tensor([-1], dtype=torch.int64)  # 0xffff... as u64
+    assert D.fold_tensor(big, 0) == (1 << 64) - 1
+
+
+def test_two_rank_gloo_shards_and_reductions(oracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda x: x["rank"])
+    whole = oracle.fixed_keys(WORLD * N_PER, 64)
+    want_total = oracle.fold64(oracle.city64_fixed(whole), 0)
+    for r in res:
+        assert r["first"] == r["rank"] * N_PER and r["n"] == N_PER
+        assert r["local"] == r["oracle_local"]          # each shard checks on its own
+        assert r["total"] == want_total                 # and they add up to the whole
+        assert r["max"] == [float(WORLD), 0.5 * (WORLD - 1)]
+        assert r["ok_all"] is False                     # one failing rank fails all
