@@ -31,7 +31,12 @@
 #include <stdint.h>
 
 #ifdef PDHT_HIP_WITH_REAL_PDHT
-#include <pdht.h>
+#ifdef PDHT_HIP_MPI_FLAVOUR
+#include <pdht.h> /* libmpipdht/pdht.h: pdht_t, pdht_hash (:236) */
+extern pdht_context_t *c; /* as libmpipdht/hash.c:4 */
+#else
+#include <pdht_impl.h> /* libpdht: pdht.h + pdht_hash (pdht_impl.h:128) + c */
+#endif
 #define PDHT_HIP_NRANKS() (c->size)
 #else
 
