@@ -199,7 +199,8 @@ constexpr u32 kHistLds = 4096;  // per-workgroup LDS bins before going global
 
 // pdht_hash placement (libpdht/hash.c:26-29) + rankputs histogram
 // (putget.c:55).
-struct SinkPlace {
+template <bool NTS = false>
+struct SinkPlaceT {
   static constexpr u32 kHist = kHistLds;
   u32 *lds_hist;  // set by the kernel
   u64 *mbits;
@@ -216,11 +217,11 @@ struct SinkPlace {
     }
   }
   __device__ __forceinline__ void put(u64 i, u64 h) {
-    mbits[i] = h;
-    if (ptindex) ptindex[i] = (u32)pt.mod(h);
+    st<NTS>(h, mbits + i);
+    if (ptindex) st<NTS>((u32)pt.mod(h), ptindex + i);
     if (rank || hist) {
       const u32 r = (u32)rk.mod(h);
-      if (rank) *reinterpret_cast<u32 *>(rank + i * rank_stride) = r;
+      if (rank) st<NTS>(r, reinterpret_cast<u32 *>(rank + i * rank_stride));
       if (hist) {
         if (nranks <= kHistLds)
           atomicAdd(lds_hist + r, 1u);
@@ -235,6 +236,14 @@ struct SinkPlace {
       for (u32 r = threadIdx.x; r < nranks; r += blockDim.x)
         if (lds_hist[r]) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)lds_hist[r]);
     }
+  }
+};
+typedef SinkPlaceT<false> SinkPlace;
+template <>
+struct NtSink<SinkPlace> {
+  typedef SinkPlaceT<true> type;
+  static __host__ type make(SinkPlace s) {
+    return type{s.lds_hist, s.mbits, s.ptindex, s.rank, s.rank_stride, s.hist, s.pt, s.rk, s.nranks};
   }
 };
 
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_lds64(const uint8_t *__restric
 // 4 contiguous 16-B pieces of the NEXT tile (global_load_dwordx4, 1 KiB per
 // wave-instruction) while the current tile hashes, then writes them into the
 // image with ds_write_b128.
-template <class Algo, class Sink, bool LNT = false>
+template <class Algo, class Sink, bool LNT = false, int DEPTH = 1>
 __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restrict__ keys, u64 n,
                                                           Algo algo, Sink sink) {
   __shared__ __attribute__((aligned(16))) u32x4 img[kWavesPerBlock][256];  // 4 KiB per wave
@@ -397,42 +406,51 @@ __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restr
   const u64 ntiles = (n + 63) >> 6;
   const u64 full = n >> 6;
   const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  u32x4 pre[4];
-  auto fetch = [&](u64 t) {
+  // DEPTH tiles of prefetch in flight per wave (register sets, static index)
+  u32x4 pre[DEPTH][4];
+  auto fetch = [&](int d, u64 t) {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(keys + (t << 12));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pre[j] = ld<LNT>(src + 64 * j + lane);
+    for (int j = 0; j < 4; ++j) pre[d][j] = ld<LNT>(src + 64 * j + lane);
   };
-  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
-  if (t < full) fetch(t);
-  for (; t < ntiles; t += nwaves) {
-    const u64 tn = t + nwaves;
-    const u64 i = (t << 6) + lane;
-    RegReader<16> r;    if (t < full) {
+  const u64 t0 = (u64)blockIdx.x * kWavesPerBlock + wave;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const u32 g = 64 * j + lane;
-        img[wave][xpose_slot(g >> 2, g & 3)] = pre[j];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (tn < full) fetch(tn);
-      const u32 sw = (lane >> 2) & 3;
+  for (int d = 0; d < DEPTH; ++d)
+    if (t0 + d * nwaves < full) fetch(d, t0 + d * nwaves);
+  for (u64 t = t0; t < ntiles; t += DEPTH * nwaves) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const u32x4 v = img[wave][4 * lane + (c ^ sw)];
-        r.d[4 * c + 0] = v.x;
-        r.d[4 * c + 1] = v.y;
-        r.d[4 * c + 2] = v.z;
-        r.d[4 * c + 3] = v.w;
+    for (int d = 0; d < DEPTH; ++d) {
+      const u64 tt = t + d * nwaves;
+      if (tt >= ntiles) break;  // wave-uniform
+      const u64 i = (tt << 6) + lane;
+      RegReader<16> r;
+      if (tt < full) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u32 g = 64 * j + lane;
+          img[wave][xpose_slot(g >> 2, g & 3)] = pre[d][j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const u64 tn = tt + DEPTH * nwaves;
+        if (tn < full) fetch(d, tn);  // refill this register set while hashing
+        const u32 sw = (lane >> 2) & 3;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const u32x4 v = img[wave][4 * lane + (c ^ sw)];
+          r.d[4 * c + 0] = v.x;
+          r.d[4 * c + 1] = v.y;
+          r.d[4 * c + 2] = v.z;
+          r.d[4 * c + 3] = v.w;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      } else if (i < n) {
+        load_key_regs<64>(keys, i, r);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    } else if (i < n) {
-      load_key_regs<64>(keys, i, r);
+      if (i < n) sink.put(i, algo(r, (u64)64));
     }
-    if (i < n) sink.put(i, algo(r, (u64)64));
   }
   sink.flush();
 }

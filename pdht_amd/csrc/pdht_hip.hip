@@ -86,6 +86,44 @@ static FastMod make_fastmod(u64 d) {
 constexpr int kWinBytes = 12288;     // k_window: LDS window per wave (12 KiB)
 constexpr int kVarWinBytes = 36864;  // k_var_sorted: per 256-key tile; 4 blocks per CU
 
+// Packed 8/16/32-byte keys: each lane loads its own key (lane-adjacent rows,
+// so 8- and 16-byte keys are fully coalesced), U keys in flight per lane.
+// Defaults from tools/placebench.py (interleaved A/B): 8-B keys with
+// non-temporal stores (+26 % on fused placement), 16-B keys with
+// non-temporal loads and stores (+6-11 %).  Variants: 16 = nt loads+stores,
+// 17 = nt stores, 18 = plain.
+template <int LMAX, class Algo, class Sink>
+static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Sink sink,
+                         hipStream_t st, int dev, u64 blocks, int variant) {
+  typedef typename NtSink<Sink>::type SinkNt;
+  const SinkNt snt = NtSink<Sink>::make(sink);
+  if constexpr (LMAX == 8) {
+    const unsigned g = grid_for((blocks + 3) / 4, 8, dev);
+    if (variant == 16) {
+      g_kernel = "k_fixed_direct<8,4,nt>";
+      k_fixed_direct<8, 4, Algo, SinkNt, true><<<g, kBlock, 0, st>>>(k, n, algo, snt);
+    } else if (variant == 18) {
+      g_kernel = "k_fixed_direct<8,4,plain>";
+      k_fixed_direct<8, 4, Algo, Sink><<<g, kBlock, 0, st>>>(k, n, algo, sink);
+    } else {
+      g_kernel = "k_fixed_direct<8,4,nt-store>";
+      k_fixed_direct<8, 4, Algo, SinkNt, false><<<g, kBlock, 0, st>>>(k, n, algo, snt);
+    }
+  } else {
+    const unsigned g = grid_for((blocks + 1) / 2, 8, dev);
+    if (keylen == 32) {
+      g_kernel = "k_fixed_direct<32,2>";
+      k_fixed_direct<32, 2, Algo, Sink><<<g, kBlock, 0, st>>>(k, n, algo, sink);
+    } else if (variant == 18 || variant == 17) {
+      g_kernel = "k_fixed_direct<16,2,plain>";
+      k_fixed_direct<16, 2, Algo, Sink><<<g, kBlock, 0, st>>>(k, n, algo, sink);
+    } else {
+      g_kernel = "k_fixed_direct<16,2,nt>";
+      k_fixed_direct<16, 2, Algo, SinkNt, true><<<g, kBlock, 0, st>>>(k, n, algo, snt);
+    }
+  }
+}
+
 // Fixed-length keys: dispatch to the register-direct / LDS-transposed kernel
 // when the length is one of the specialised ones and the layout allows it,
 // else to the generic window kernel.
@@ -136,24 +174,29 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
         g_kernel = "k_fixed_direct<64,1,nt-store>";
         k_fixed_direct<64, 1, Algo, SinkNt, false><<<g1, kBlock, 0, st>>>(k, n, algo, sink_nt);
         break;
+      case 15:
+        g_kernel = "k_fixed_xpose64<depth2>";
+        k_fixed_xpose64<Algo, SinkNt, true, 2><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
+        break;
       case 1:
         g_kernel = "k_fixed_xpose64<plain>";
         k_fixed_xpose64<Algo, Sink, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink);
         break;
-      default:  // 0: measured fastest (tools/kbench.py)
-        g_kernel = "k_fixed_xpose64";
+      case 7:
+        g_kernel = "k_fixed_xpose64<depth1>";
         k_fixed_xpose64<Algo, SinkNt, true><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
         break;
+      default:  // 0: measured fastest (tools/kbench.py): nt/nt,
+                // two tiles of prefetch in flight per wave, 3 workgroups per CU
+        g_kernel = "k_fixed_xpose64";
+        k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+            k, n, algo, sink_nt);
+        break;
     }
-  } else if (packed && keylen == 32 && al16 && variant != 3) {
-    g_kernel = "k_fixed_direct<32,2>";
-    k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
-  } else if (packed && keylen == 16 && al16 && variant != 3) {
-    g_kernel = "k_fixed_direct<16,2>";
-    k_fixed_direct<16, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+  } else if (packed && (keylen == 32 || keylen == 16) && al16 && variant != 3) {
+    launch_small<32>(keylen, k, n, algo, sink, st, dev, blocks, variant);
   } else if (packed && keylen == 8 && al8 && variant != 3) {
-    g_kernel = "k_fixed_direct<8,4>";
-    k_fixed_direct<8, 4, Algo, Sink><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo, sink);
+    launch_small<8>(keylen, k, n, algo, sink, st, dev, blocks, variant);
   } else {
     const u64 tiles = (n + 63) / 64;
     if (variant == 3) {

@@ -106,8 +106,9 @@ def test_seeded_batches(dev, oracle, L):
 VARIANT_KERNELS = {0: "k_fixed_xpose64", 1: "k_fixed_xpose64<plain>", 2: "k_fixed_lds64",
                    3: "k_window<fixed>",
                    4: "k_fixed_lds64<nt-store>", 5: "k_fixed_direct<64,1,nt-load,nt-store>",
-                   6: "k_fixed_direct<64,1>", 7: "k_fixed_xpose64<nt-load,nt-store>",
-                   8: "k_fixed_xpose64<nt-store>", 9: "k_fixed_direct<64,1,nt-store>"}
+                   6: "k_fixed_direct<64,1>", 7: "k_fixed_xpose64<depth1>",
+                   8: "k_fixed_xpose64<nt-store>", 9: "k_fixed_direct<64,1,nt-store>",
+                   15: "k_fixed_xpose64<depth2>"}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANT_KERNELS))
@@ -243,6 +244,26 @@ def test_place_batch(dev, oracle, L, nptes, nranks):
     assert (rk.cpu().numpy().view(np.uint32) == r2).all()
     if hist is not None:
         assert (hist.cpu().numpy() == np.bincount(r2, minlength=nranks)).all()
+
+
+@pytest.mark.parametrize("L", [8, 16, 32])
+@pytest.mark.parametrize("variant", [0, 16, 17, 18])
+def test_small_key_variants(dev, oracle, L, variant):
+    rng = np.random.default_rng(L + variant)
+    k = rng.integers(0, 256, (70001, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    old = P.set_variant(variant)
+    try:
+        got = u64(P.city64_batch(kd))
+        assert P.last_kernel().startswith(f"k_fixed_direct<{L},")
+        mb, pt, rk = P.place_batch(kd, 7, 1000)
+    finally:
+        P.set_variant(old)
+    assert (got == oracle.city64_fixed(k)).all()
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 7, 1000)
+    assert (u64(mb) == m2).all()
+    assert (pt.cpu().numpy().view(np.uint32) == p2).all()
+    assert (rk.cpu().numpy().view(np.uint32) == r2).all()
 
 
 def test_place_golden_u64_keys(dev, golden):

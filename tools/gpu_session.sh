@@ -17,6 +17,10 @@ for step in "$@"; do
              tail -1 gpurun_out/bench_$cfg.log ;;
     kbench)  timeout -k 10 300 python tools/kbench.py > gpurun_out/kbench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/kbench.log | cut -c1-200 ;;
+    kbench_pc) timeout -k 10 400 python tools/kbench.py --variants 0,15 --per-cu 3,4,5 --rounds 7 > gpurun_out/kbench_pc.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/kbench_pc.log | cut -c1-200 ;;
+    kbench_crc_pc) timeout -k 10 400 python tools/kbench.py --algo crc128 --variants 0,15 --per-cu 2,4,6 --rounds 5 > gpurun_out/kbench_crc_pc.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/kbench_crc_pc.log | cut -c1-200 ;;
     kbench_crc) timeout -k 10 300 python tools/kbench.py --algo crc128 > gpurun_out/kbench_crc.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/kbench_crc.log | cut -c1-200 ;;
     prof)    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host > gpurun_out/prof.log 2>&1; rc=$?
@@ -29,6 +33,8 @@ for step in "$@"; do
              tail -3 gpurun_out/gpu_vartests.log ;;
     varbench) timeout -k 10 300 python tools/varbench.py --variants ${VARIANTS:-0,11,12,13,14,10} > gpurun_out/varbench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/varbench.log ;;
+    placebench) timeout -k 10 300 python tools/placebench.py > gpurun_out/placebench.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/placebench.log | cut -c1-220 ;;
     counters) timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; rc=$?; rc=0 ;;
     sq_*)    cfg=${step#sq_}
              timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sq_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/sq_$cfg.log 2>&1; rc=$?

@@ -16,9 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import pdht_amd as P  # noqa: E402
 
-NAMES = {0: "xpose nt-load nt-store (default)", 1: "xpose plain", 2: "lds-dma+prefetch", 3: "window",
-         4: "lds-dma nt-store", 5: "direct nt-load nt-store", 6: "direct plain",
-         7: "xpose nt-load nt-store", 8: "xpose nt-store", 9: "direct nt-store"}
+NAMES = {0: "xpose nt/nt depth 2, 3 WG/CU (default)", 1: "xpose plain", 2: "lds-dma+prefetch",
+         3: "window", 4: "lds-dma nt-store", 5: "direct nt-load nt-store", 6: "direct plain",
+         7: "xpose nt/nt depth 1, 4 WG/CU", 8: "xpose nt-store", 9: "direct nt-store",
+         15: "xpose nt/nt depth 2, 4 WG/CU"}
 
 
 def main():
