@@ -162,10 +162,6 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
         g_kernel = "k_fixed_direct<64,1>";
         k_fixed_direct<64, 1, Algo, Sink, false><<<g1, kBlock, 0, st>>>(k, n, algo, sink);
         break;
-      case 7:
-        g_kernel = "k_fixed_xpose64<nt-load,nt-store>";
-        k_fixed_xpose64<Algo, SinkNt, true><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
       case 8:
         g_kernel = "k_fixed_xpose64<nt-store>";
         k_fixed_xpose64<Algo, SinkNt, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
