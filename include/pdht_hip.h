@@ -100,6 +100,23 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
                          uint32_t *ptindex, void *rank, size_t rank_stride,
                          uint64_t *hist, pdht_hip_stream_t stream);
 
+/* Destination bucketing (the shape of the Meraculous
+ * loader, bench/Meraculous/buildUFXhashBinary.h:83-112): a stable counting
+ * sort of n packed keysize-byte keys by rank = CityHash64 % nranks.  Bucket
+ * r occupies positions [bucket_offsets[r], bucket_offsets[r+1]) of the
+ * outputs, keys in their original order; bucket_offsets has nranks+1
+ * entries.  Outputs at bucketed positions: mbits_out (required),
+ * keys_out (keysize bytes per key), ptindex_out (% nptes), index_out
+ * (original key index) -- each optional (NULL).  nranks <= 8192,
+ * n < 2^32.  `workspace` (device) must hold pdht_bucket_workspace_bytes. */
+size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks);
+int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
+                          uint32_t nptes, uint32_t nranks, void *workspace,
+                          size_t workspace_bytes, void *keys_out,
+                          uint64_t *mbits_out, uint32_t *ptindex_out,
+                          uint64_t *index_out, uint64_t *bucket_offsets,
+                          pdht_hip_stream_t stream);
+
 /* ---- host-resident batches ---------------------------------------------- */
 /* Keys and digests in host memory.  Chunks are copied H2D, hashed and copied
  * back D2H on several streams so copies and kernels overlap; pinned

@@ -100,6 +100,8 @@ def _declare(L):
         "pdht_hip_splitmix64_fill_dev": (C.c_int, [_U64, _U64, _S, _V, _V]),
         "pdht_hip_mixed_lengths_dev": (C.c_int, [_U64, _U64, _S, _U32, _U32, _V, _V]),
         "pdht_hip_read_stream_dev": (C.c_int, [_V, _S, C.c_int, _V, _V]),
+        "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _U32]),
+        "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
         "CityHash64": (_U64, [_V, _S]),
         "CityHash64WithSeed": (_U64, [_V, _S, _U64]),
         "CityHash64WithSeeds": (_U64, [_V, _S, _U64, _U64]),
@@ -358,6 +360,34 @@ def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=
                                       _dptr(hist) if hist is not None else None,
                                       _stream_ptr(stream)), "pdht_place_batch_dev")
     return mb, pt, rk
+
+
+def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=True,
+                 with_index=True, stream=None):
+    """Destination bucketing (include/pdht_hip.h pdht_bucket_batch_dev): a stable
+    counting sort of packed keys [n, L] by rank = CityHash64 % nranks.
+
+    Returns (keys_out [n, L] | None, mbits int64[n], ptindex int32[n] | None,
+    index int64[n] | None, offsets int64[nranks+1]); bucket r is rows
+    offsets[r]:offsets[r+1], keys in original order.
+    """
+    torch = _torch()
+    n, L, stride = _keys_2d(keys)
+    if stride != L:
+        raise ValueError("bucket_batch needs packed keys")
+    dev = keys.device
+    ws_bytes = lib().pdht_bucket_workspace_bytes(n, nranks)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    ko = torch.empty_like(keys) if with_keys else None
+    mb = torch.empty(n, dtype=torch.int64, device=dev)
+    pt = torch.empty(n, dtype=torch.int32, device=dev) if with_ptindex else None
+    ix = torch.empty(n, dtype=torch.int64, device=dev) if with_index else None
+    offs = torch.empty(nranks + 1, dtype=torch.int64, device=dev)
+    p = lambda t: _dptr(t) if t is not None else None  # noqa: E731
+    _check(lib().pdht_bucket_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(ws), ws_bytes, p(ko),
+                                       _dptr(mb), p(pt), p(ix), _dptr(offs), _stream_ptr(stream)),
+           "pdht_bucket_batch_dev")
+    return ko, mb, pt, ix, offs
 
 
 def splitmix64_fill(seed: int, first: int, nwords: int, out=None, device="cuda", stream=None):

@@ -196,6 +196,8 @@ struct FastMod {
 };
 
 constexpr u32 kHistLds = 4096;  // per-workgroup LDS bins before going global
+constexpr u32 kHistPartHdr = 64;  // u32 words before the partial rows (word 0 = rows written)
+constexpr u32 kHistRedRows = 64;  // partial rows folded per k_hist_reduce thread
 
 // pdht_hash placement (libpdht/hash.c:26-29) + rankputs histogram
 // (putget.c:55).
@@ -210,6 +212,8 @@ struct SinkPlaceT {
   u64 *hist;
   FastMod pt, rk;
   u32 nranks;
+  u32 *part;     // per-workgroup partial rows (k_hist_reduce), or NULL
+  u32 part_cap;  // rows available in `part`
   __device__ __forceinline__ void init() {
     if (hist && nranks <= kHistLds) {
       for (u32 r = threadIdx.x; r < nranks; r += blockDim.x) lds_hist[r] = 0;
@@ -233,17 +237,40 @@ struct SinkPlaceT {
   __device__ __forceinline__ void flush() {
     if (hist && nranks <= kHistLds) {
       __syncthreads();
-      for (u32 r = threadIdx.x; r < nranks; r += blockDim.x)
-        if (lds_hist[r]) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)lds_hist[r]);
+      if (part && blockIdx.x < part_cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) part[0] = gridDim.x;
+        u32 *row = part + kHistPartHdr + (u64)blockIdx.x * nranks;
+        for (u32 r = threadIdx.x; r < nranks; r += blockDim.x) row[r] = lds_hist[r];
+      } else {
+        for (u32 r = threadIdx.x; r < nranks; r += blockDim.x)
+          if (lds_hist[r]) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)lds_hist[r]);
+      }
     }
   }
 };
+
+// Folds the partial rows of the first min(gridDim of the placement launch,
+// cap) workgroups into hist: thread = bin, blockIdx.y = a run of rows.
+__global__ __launch_bounds__(kBlock) void k_hist_reduce(const u32 *__restrict__ part, u32 cap,
+                                                        u32 nranks, u64 *__restrict__ hist) {
+  const u32 rows = min(part[0], cap);
+  const u32 r = blockIdx.x * kBlock + threadIdx.x;
+  const u32 b0 = blockIdx.y * kHistRedRows;
+  if (r >= nranks || b0 >= rows) return;
+  const u32 b1 = min(rows, b0 + kHistRedRows);
+  const u32 *p = part + kHistPartHdr + (u64)b0 * nranks + r;
+  u64 sum = 0;
+#pragma unroll 16
+  for (u32 b = b0; b < b1; ++b, p += nranks) sum += *p;
+  if (sum) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)sum);
+}
 typedef SinkPlaceT<false> SinkPlace;
 template <>
 struct NtSink<SinkPlace> {
   typedef SinkPlaceT<true> type;
   static __host__ type make(SinkPlace s) {
-    return type{s.lds_hist, s.mbits, s.ptindex, s.rank, s.rank_stride, s.hist, s.pt, s.rk, s.nranks};
+    return type{s.lds_hist, s.mbits, s.ptindex, s.rank, s.rank_stride, s.hist, s.pt, s.rk, s.nranks,
+                s.part, s.part_cap};
   }
 };
 
@@ -464,8 +491,12 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
                                                    Sink sink) {
-  static_assert(WIN % 1024 == 0, "window = whole 1 KiB DMA pieces");
-  __shared__ __attribute__((aligned(16))) u32 win[kWavesPerBlock][WIN / 4 + 4];
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  // Windows of the 4 waves back to back; a span's trailing dword read may run
+  // past a window's end only when it is not used (aligned span), so only the
+  // array as a whole needs the 16 B of slack.  WIN need not be a multiple of
+  // 1 KiB: 10224 B keeps a workgroup under 40 KiB = 4 workgroups per CU.
+  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
   sink.init();
@@ -473,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
   const u32 lane = threadIdx.x & 63;
   const u64 ntiles = (n + 63) >> 6;
   const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  u32 *lds = win[wave];
+  u32 *lds = win_all + wave * (WIN / 4);
   for (u64 t = (u64)blockIdx.x * kWavesPerBlock + wave; t < ntiles; t += nwaves) {
     const u64 k0 = t << 6;
     const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;  // one past the tile's last key
@@ -507,7 +538,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
     // 16-B-aligned pieces never cross a page the key bytes do not touch.
     const uint8_t *src = bytes + wlo;
 #pragma unroll
-    for (int j = 0; j < WIN / 1024; ++j) {
+    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
       if ((u32)j * 1024 < wbytes) {  // wave-uniform
         if ((u32)j * 1024 + lane * 16 < wbytes)
           __builtin_amdgcn_global_load_lds(

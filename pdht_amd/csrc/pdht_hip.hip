@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/pdht_hip.h"
+#include "bucket.h"
 #include "kernels.h"
 
 #define PDHT_API extern "C" __attribute__((visibility("default")))
@@ -49,6 +50,12 @@ static int current_device(int *dev) {
   DevInfo &d = g_dev[*dev];
   std::call_once(d.once, [&] {
     d.err = hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, *dev);
+    // stream-ordered scratch (histogram partials) stays cached in the pool
+    hipMemPool_t pool;
+    if (d.err == hipSuccess && hipDeviceGetDefaultMemPool(&pool, *dev) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
   });
   if (d.err != hipSuccess) return fail("%s (querying CU count)", hipGetErrorString(d.err));
   return 0;
@@ -238,8 +245,8 @@ static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n
             b, offsets, obase, 0, 0, n, algo, sink);
         break;
       case 12:
-        g_kernel = "k_window<var,nt,8K>";
-        k_window<8192, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+        g_kernel = "k_window<var,nt,10224>";
+        k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
             b, offsets, obase, 0, 0, n, algo, sink_nt);
         break;
       case 13:
@@ -527,8 +534,31 @@ PDHT_API int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n, ui
                                   uint32_t nranks, uint64_t *mbits, uint32_t *ptindex, void *rank,
                                   size_t rank_stride, uint64_t *hist, pdht_hip_stream_t s) {
   if (int rc = check_place(n, mbits, nptes, nranks, rank, rank_stride)) return rc;
-  return launch_fixed(keys, keysize, keysize, n, AlgoCity64{},
-                      make_place_sink(mbits, ptindex, rank, rank_stride, hist, nptes, nranks), ST(s));
+  SinkPlace sink = make_place_sink(mbits, ptindex, rank, rank_stride, hist, nptes, nranks);
+  if (!hist || nranks > kHistLds || n == 0 || g_variant.load(std::memory_order_relaxed) == 19)
+    return launch_fixed(keys, keysize, keysize, n, AlgoCity64{}, sink, ST(s));
+  // Two-level rankputs histogram: each workgroup stores its LDS counts as a
+  // partial row; k_hist_reduce folds the rows into `hist` with one atomic per
+  // bin per 64 rows.  A global atomic per bin per workgroup (variant 19) puts
+  // thousands of same-address device-scope atomics on every bin at the end of
+  // the launch.
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  const u32 cap = (u32)std::max(1, g_dev[dev].cus) * (u32)std::max(16, env_int("PDHT_HIP_BLOCKS_PER_CU", 0));
+  const size_t bytes = ((size_t)kHistPartHdr + (size_t)cap * nranks) * sizeof(u32);
+  void *part = nullptr;
+  HIP_TRY(hipMallocAsync(&part, bytes, ST(s)));
+  sink.part = static_cast<u32 *>(part);
+  sink.part_cap = cap;
+  int rc = launch_fixed(keys, keysize, keysize, n, AlgoCity64{}, sink, ST(s));
+  if (rc == 0) {
+    const dim3 grid((nranks + kBlock - 1) / kBlock, (cap + kHistRedRows - 1) / kHistRedRows);
+    k_hist_reduce<<<grid, kBlock, 0, ST(s)>>>(sink.part, cap, nranks, hist);
+    if (hipGetLastError() != hipSuccess) rc = fail("k_hist_reduce launch failed%s", "");
+  }
+  const hipError_t e = hipFreeAsync(part, ST(s));
+  if (rc == 0 && e != hipSuccess) return fail("%s (hipFreeAsync)", hipGetErrorString(e));
+  return rc;
 }
 
 // -------------------------------------------------------- host batches ---
@@ -725,6 +755,72 @@ PDHT_API int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
   if (int rc = current_device(&dev)) return rc;
   k_mixed_lengths<<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, ST(s)>>>(
       seed, first, n, lo, hi - lo + 1, lens);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------- destination bucketing ---
+namespace pdht {
+struct BucketWs {
+  u32 *counts;
+  u64 *totals, *base;
+  size_t bytes;
+};
+static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
+static BucketWs bucket_layout(void *ws, size_t n, u32 nranks) {
+  const u64 ntiles = (n + kBucketTile - 1) / kBucketTile;
+  BucketWs w{};
+  uint8_t *p = static_cast<uint8_t *>(ws);
+  size_t off = 0;
+  w.counts = reinterpret_cast<u32 *>(p + off);
+  off += round256((size_t)nranks * ntiles * 4);
+  w.totals = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)nranks * 8);
+  w.base = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)nranks * 8);
+  w.bytes = off;
+  return w;
+}
+}  // namespace pdht
+
+PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
+  return bucket_layout(nullptr, n, nranks).bytes;
+}
+
+PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
+                                   uint32_t nranks, void *workspace, size_t workspace_bytes,
+                                   void *keys_out, uint64_t *mbits_out, uint32_t *ptindex_out,
+                                   uint64_t *index_out, uint64_t *bucket_offsets,
+                                   pdht_hip_stream_t s) {
+  if (int rc = check_place(n, mbits_out, nptes, nranks, nullptr, 0)) return rc;
+  if (nranks > kBucketMaxRanks) return fail("bucketing supports up to 8192 ranks%s", "");
+  if (n >= (1ull << 32)) return fail("bucketing: n must be < 2^32 per call%s", "");
+  if (!bucket_offsets) return fail("bucket_offsets must not be NULL%s", "");
+  if (n && (!keys || keysize == 0)) return fail("null keys or zero keysize%s", "");
+  const BucketWs w = bucket_layout(workspace, n, nranks);
+  if (!workspace || workspace_bytes < w.bytes) return fail("workspace too small%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  hipStream_t st = ST(s);
+  const u64 ntiles = (n + kBucketTile - 1) / kBucketTile;
+  const FastMod pt = make_fastmod(nptes), rk = make_fastmod(nranks);
+  u32 nbits = 0;
+  while ((1u << nbits) < nranks) ++nbits;
+  const uint8_t *k = static_cast<const uint8_t *>(keys);
+  const size_t lds = (size_t)nranks * 4;
+  g_kernel = "k_bucket";
+  if (ntiles) {
+    k_bucket_count<<<grid_for(ntiles, 8, dev), kBlock, lds, st>>>(k, (u32)keysize, n, rk, nranks,
+                                                                  w.counts, ntiles);
+    k_bucket_scan<<<nranks, kBlock, 0, st>>>(w.counts, ntiles, w.totals);
+  } else {
+    HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
+  }
+  k_bucket_base<<<1, kBlock, 0, st>>>(w.totals, nranks, w.base, bucket_offsets);
+  if (ntiles)
+    k_bucket_scatter<<<grid_for(ntiles, 16, dev), 64, lds, st>>>(
+        k, (u32)keysize, n, pt, rk, nranks, nbits, w.counts, w.base, ntiles,
+        static_cast<uint8_t *>(keys_out), mbits_out, ptindex_out, index_out);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -89,6 +89,40 @@ def allreduce_min_flag(ok: bool, device=None) -> bool:
     return bool(int(t.item()))
 
 
+def exchange_buckets(keys_out, mbits_out, offsets, index_out=None):
+    """Ship every bucket to its owner rank: bucket r of this rank (rows
+    offsets[r]:offsets[r+1] of the bucketed outputs, pdht_amd.bucket_batch
+    with nranks == world size) goes to rank r with one all-to-all(v) per
+    payload (RCCL over xGMI on GPUs, gloo on CPU).
+
+    Returns (keys [m, L], mbits [m], index [m] | None, recv_counts [world]):
+    all keys this rank owns (mbits % world == rank), grouped by source rank in
+    rank order, each group in its source's key order.  The only collective on
+    the placement path: the first step that needs one.
+    """
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    if offsets.numel() != world + 1:
+        raise ValueError("bucket_batch must have been called with nranks == world size")
+    send = (offsets[1:] - offsets[:-1]).to(torch.int64)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    s_split = [int(x) for x in send.cpu().tolist()]
+    r_split = [int(x) for x in recv.cpu().tolist()]
+    m = sum(r_split)
+
+    def a2a(t):
+        out = torch.empty((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_to_all_single(out, t.contiguous(), r_split, s_split)
+        return out
+
+    keys = a2a(keys_out) if keys_out is not None else None
+    mbits = a2a(mbits_out)
+    index = a2a(index_out) if index_out is not None else None
+    return keys, mbits, index, recv
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:

@@ -49,10 +49,22 @@ def _worker(rank, world, port, q):
         total = D.allreduce_fold(local)
         mx = D.allreduce_max([float(r + 1), 0.5 * r])
         ok_all = D.allreduce_min_flag(r != 1)  # rank 1 reports failure
+        # f4 exchange: bucket this shard by owner rank (on a GPU pdht_amd.bucket_batch
+        # does this; here the oracle's placement + a stable sort stands in) and ship
+        # every bucket to its owner
+        mb, _, rk = O.pdht_hash_fixed(keys[:, :8], 3, w)
+        order = np.argsort(rk, kind="stable")
+        offs = np.concatenate([[0], np.cumsum(np.bincount(rk, minlength=w))])
+        gidx = torch.from_numpy((order + sh.first).astype(np.int64))
+        k2, m2, i2, cnt = D.exchange_buckets(torch.from_numpy(keys[order, :8].copy()),
+                                             torch.from_numpy(mb[order].view(np.int64)),
+                                             torch.from_numpy(offs.astype(np.int64)), gidx)
         D.barrier()
         q.put({"rank": r, "first": sh.first, "n": sh.n, "local": local, "total": total,
                "max": mx, "ok_all": ok_all,
-               "oracle_local": O.fold64(O.city64_fixed(keys), sh.first)})
+               "oracle_local": O.fold64(O.city64_fixed(keys), sh.first),
+               "xkeys": k2.numpy(), "xmbits": m2.numpy().view(np.uint64), "xidx": i2.numpy(),
+               "xcnt": cnt.numpy()})
     finally:
         dist.destroy_process_group()
 
@@ -91,3 +103,13 @@ def test_two_rank_gloo_shards_and_reductions(oracle):
         assert r["total"] == want_total                 # and they add up to the whole
         assert r["max"] == [float(WORLD), 0.5 * (WORLD - 1)]
         assert r["ok_all"] is False                     # one failing rank fails all
+    # after the exchange rank r holds exactly the keys the reference places on r,
+    # grouped by source rank, each group in key order
+    mb, _, rk = oracle.pdht_hash_fixed(whole[:, :8], 3, WORLD)
+    for r in res:
+        want = np.flatnonzero(rk == r["rank"])
+        assert (r["xidx"] == want).all()
+        assert (r["xmbits"] == mb[want]).all()
+        assert (r["xkeys"] == whole[want, :8]).all()
+        assert list(r["xcnt"]) == [int(((rk == r["rank"]) & (np.arange(len(rk)) // N_PER == s)).sum())
+                                   for s in range(WORLD)]

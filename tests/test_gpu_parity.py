@@ -186,7 +186,7 @@ def test_var_golden_mixed(dev, golden, oracle):
 
 
 VAR_KERNELS = {0: "k_window<var,nt>", 3: "k_window<var>", 10: "k_var_sorted",
-               11: "k_window<var,nt>", 12: "k_window<var,nt,8K>", 13: "k_window<var,nt,16K>",
+               11: "k_window<var,nt>", 12: "k_window<var,nt,10224>", 13: "k_window<var,nt,16K>",
                14: "k_window_pf<var>"}
 
 
@@ -246,6 +246,25 @@ def test_place_batch(dev, oracle, L, nptes, nranks):
         assert (hist.cpu().numpy() == np.bincount(r2, minlength=nranks)).all()
 
 
+@pytest.mark.parametrize("L", [8, 64])
+@pytest.mark.parametrize("variant", [0, 19])  # 0: two-level histogram, 19: per-workgroup atomics
+def test_place_hist_many_workgroups(dev, oracle, L, variant):
+    # enough keys for a full persistent grid; hist accumulates across calls
+    rng = np.random.default_rng(L + 5)
+    k = rng.integers(0, 256, (1 << 21, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    hist = torch.full((1000,), 5, dtype=torch.int64, device=dev)
+    old = P.set_variant(variant)
+    try:
+        P.place_batch(kd, 3, 1000, hist=hist)
+        P.place_batch(kd[:12345], 3, 1000, hist=hist)
+    finally:
+        P.set_variant(old)
+    _, _, r2 = oracle.pdht_hash_fixed(k, 3, 1000)
+    want = 5 + np.bincount(r2, minlength=1000) + np.bincount(r2[:12345], minlength=1000)
+    assert (hist.cpu().numpy() == want).all()
+
+
 @pytest.mark.parametrize("L", [8, 16, 32])
 @pytest.mark.parametrize("variant", [0, 16, 17, 18])
 def test_small_key_variants(dev, oracle, L, variant):
@@ -264,6 +283,24 @@ def test_small_key_variants(dev, oracle, L, variant):
     assert (u64(mb) == m2).all()
     assert (pt.cpu().numpy().view(np.uint32) == p2).all()
     assert (rk.cpu().numpy().view(np.uint32) == r2).all()
+
+
+@pytest.mark.parametrize("L", [8, 13, 64])
+@pytest.mark.parametrize("nranks", [1, 2, 7, 1000, 8192])
+@pytest.mark.parametrize("n", [0, 1, 4095, 100003])
+def test_bucket_batch(dev, oracle, L, nranks, n):
+    rng = np.random.default_rng(L * 7 + nranks + n)
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    ko, mb, pt, ix, offs = P.bucket_batch(to_dev(k, dev), 3, nranks)
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, nranks) if n else (
+        np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+    order = np.argsort(r2, kind="stable")  # the reference placement, stably bucketed
+    assert (ix.cpu().numpy() == order).all()
+    assert (u64(mb) == m2[order]).all()
+    assert (pt.cpu().numpy().view(np.uint32) == p2[order]).all()
+    assert (ko.cpu().numpy() == k[order]).all()
+    want_offs = np.concatenate([[0], np.cumsum(np.bincount(r2, minlength=nranks))])
+    assert (offs.cpu().numpy() == want_offs).all()
 
 
 def test_place_golden_u64_keys(dev, golden):

@@ -31,9 +31,13 @@ for step in "$@"; do
              done ;;
     vartests) timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider -k "var or cfg3 or host or smoke" > gpurun_out/gpu_vartests.log 2>&1; rc=$?
              tail -3 gpurun_out/gpu_vartests.log ;;
-    varbench) timeout -k 10 300 python tools/varbench.py --variants ${VARIANTS:-0,11,12,13,14,10} > gpurun_out/varbench.log 2>&1; rc=$?
+    ktests)  timeout -k 10 300 python -m pytest tests -m gpu -x -q -p no:cacheprovider -k "$K" > gpurun_out/gpu_ktests.log 2>&1; rc=$?
+             tail -15 gpurun_out/gpu_ktests.log | cut -c1-300 ;;
+    varbench)timeout -k 10 300 python tools/varbench.py --variants ${VARIANTS:-0,11,12,13,14,10} > gpurun_out/varbench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/varbench.log ;;
-    placebench) timeout -k 10 300 python tools/placebench.py > gpurun_out/placebench.log 2>&1; rc=$?
+    torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-host > gpurun_out/torchrun1.log 2>&1; rc=$?
+             tail -1 gpurun_out/torchrun1.log | cut -c1-400 ;;
+    placebench) timeout -k 10 300 python tools/placebench.py --variants ${PVARIANTS:-0,16,17} > gpurun_out/placebench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/placebench.log | cut -c1-220 ;;
     counters) timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; rc=$?; rc=0 ;;
     sq_*)    cfg=${step#sq_}
