@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "place"])
+    ap.add_argument("--config", default="cfg2",
+                    choices=["cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (tools/kbench.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -94,7 +95,31 @@ def main():
     cfg = a.config
     # ---------------------------------------------------------- workload ---
     keys = out = data = offs = None
-    if cfg in ("cfg2", "cfg4", "cfg5", "place"):
+    bucketed = None
+    if cfg in ("bucket", "exchange"):
+        # f4: stable counting sort of 8-B keys by destination rank (keys, mbits,
+        # ptindex, original index written at bucketed positions); "exchange"
+        # buckets by the world size and ships each bucket to its owner with
+        # all-to-all(v) (RCCL), inside the timed step
+        L = 8
+        n = a.keys_per_gpu or 16 * M
+        sh = D.weak_shard(rank, world, n)
+        words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
+        keys = words.view(torch.uint8).view(n, L)
+        nr = 1024 if cfg == "bucket" else world
+        bucketed = {"nranks": nr}
+
+        def step():
+            ko, mb, pt, ix, offs_ = P.bucket_batch(keys, 3, nr, with_ptindex=cfg == "bucket")
+            bucketed.update(ko=ko, mb=mb, pt=pt, ix=ix, offs=offs_)
+            if cfg == "exchange" and world > 1:
+                bucketed["x"] = D.exchange_buckets(ko, mb, offs_, ix + sh.first)
+        out = None
+        bytes_per_key = L + L + 8 + 8 + (4 if cfg == "bucket" else 0)
+        workload = (f"{cfg}: destination bucketing of {n >> 20}M x 8B keys per GPU by "
+                    f"CityHash64 % {nr}" + (" + all-to-all(v) exchange" if cfg == "exchange" else ""))
+        total_bytes_in = n * L
+    elif cfg in ("cfg2", "cfg4", "cfg5", "place"):
         L = 8 if cfg == "place" else 64
         n = a.keys_per_gpu or (128 * M if cfg == "cfg5" else 16 * M)
         sh = D.weak_shard(rank, world, n)
@@ -174,7 +199,10 @@ def main():
         calib = round(keys.numel() / (cms / 1e3) / 1e9, 1)
 
     # ------------------------------------------------------------ parity ---
-    parity = check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev)
+    if bucketed is not None:
+        parity = check_buckets(P, torch, D, sh, keys, bucketed, dev)
+    else:
+        parity = check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev)
 
     # ------------------------------------------------------- report ------
     value = n * world * a.steps / elapsed / 1e9
@@ -283,6 +311,53 @@ def check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev):
         fold_ok = D.fold_tensor(out, first_idx) == want
         msgs.append(f"full-shard fold {'==' if fold_ok else '!='} reference golden ({what})")
     all_ok = D.allreduce_min_flag(bool(ok) and fold_ok, device=dev)
+    if sh.world > 1:
+        msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
+    return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
+
+
+def check_buckets(P, torch, D, sh, keys, b, dev):
+    """Bucketing checks: a sample of buckets against the oracle's placement
+    (stable order), and full-size properties on the device -- index is a
+    permutation, ranks are non-decreasing, indices increase inside a bucket,
+    keys_out == keys[index], mbits == CityHash64(keys_out)."""
+    try:
+        from oracle import oracle as O
+    except Exception as e:  # pragma: no cover
+        return f"unchecked (oracle unavailable: {e})"
+    nr, ko, mb, ix, offs = b["nranks"], b["ko"], b["mb"], b["ix"], b["offs"]
+    n = ix.numel()
+    msgs = []
+    s = min(n, 65536)
+    ks = O.fixed_keys(s, 8, first_key=sh.first)
+    m2, _, r2 = O.pdht_hash_fixed(ks, 3, nr)
+    order = np.argsort(r2, kind="stable")
+    # positions of the sample keys (index < s) inside the full bucketed output
+    ixc = ix.cpu().numpy()
+    sel = ixc < s
+    ok = bool((ixc[sel] == order).all() and (mb.cpu().numpy().view(np.uint64)[sel] == m2[order]).all())
+    msgs.append(f"first {s} keys bucketed as the oracle {'ok' if ok else 'MISMATCH'}")
+    srt = torch.sort(ix).values
+    perm = bool((srt == torch.arange(n, device=dev)).all().item())
+    same = bool((ko == keys[ix]).all().item()) and bool((P.city64_batch(ko) == mb).all().item())
+    cnt = (offs[1:] - offs[:-1])
+    rk = torch.repeat_interleave(torch.arange(nr, device=dev), cnt)
+    prop = perm and same and int(offs[-1].item()) == n
+    if n > 1:
+        prop = prop and bool(((ix[1:] > ix[:-1]) | (rk[1:] > rk[:-1])).all().item())
+    msgs.append(f"full batch: permutation, stable buckets, keys/mbits consistent {'ok' if prop else 'FAILED'}")
+    ok = ok and prop
+    if "x" in b:
+        xk, xm, xi, _ = b["x"]
+        got_m = xm.cpu().numpy().view(np.uint64)
+        mine = bool((got_m % np.uint64(sh.world) == np.uint64(sh.rank)).all())
+        mine = mine and bool((P.city64_batch(xk) == xm).all().item())
+        xk_np, xi_np = xk.cpu().numpy(), xi.cpu().numpy()
+        for j in range(0, xi.numel(), max(1, xi.numel() // 256)):  # received key j is global key xi[j]
+            mine = mine and bool((xk_np[j] == O.fixed_keys(1, 8, first_key=int(xi_np[j]))[0]).all())
+        msgs.append(f"exchange: {xi.numel()} keys received, all owned by this rank {'ok' if mine else 'FAILED'}")
+        ok = ok and mine
+    all_ok = D.allreduce_min_flag(ok, device=dev)
     if sh.world > 1:
         msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
     return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)

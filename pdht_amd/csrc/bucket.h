@@ -2,83 +2,160 @@
 //
 // The bulk loader of bench/Meraculous/buildUFXhashBinary.h:83-112 hashes
 // every key, counts keys per destination rank (my_heap_sizes[]) and later
-// ships each key to its rank.  On the GPU that is a counting sort of the
-// batch by rank = CityHash64(key) % nranks (libpdht/hash.c:26-29):
+// ships each key to its rank.  On the GPU that is a stable counting sort of
+// the batch by rank = CityHash64(key) % nranks (libpdht/hash.c:26-29):
 //
-//   k_bucket_count   per 4096-key tile: LDS histogram of ranks
-//                    -> counts[rank][tile]
-//   k_bucket_scan    per rank: exclusive scan over tiles (in place) + total
-//   k_bucket_base    exclusive scan of the totals -> bucket offsets
-//   k_bucket_scatter per tile, one wave, key groups of 64 in index order:
-//                    lanes with the same rank find each other with
-//                    ceil(log2 nranks) ballots; the group leader advances the
-//                    bucket's running position in LDS.  Keys, digests,
-//                    PTE indices and original indices land at their bucket
-//                    position.
+//   k_bucket_count*    per tile: LDS histogram of ranks -> counts[tile][rank]
+//                      (tile-major, so every tile reads/writes one coalesced row)
+//   k_bucket_colscan   per (64 ranks, chunk of 32 tiles): exclusive scan down
+//                      the chunk in place, chunk sum -> chunks[chunk][rank]
+//   k_bucket_chunkscan per rank: exclusive scan over chunks in place + total
+//   k_bucket_base      exclusive scan of the totals -> bucket offsets
+//   k_bucket_scatter*  per tile: the tile's first slot in bucket r is
+//                      base[r] + chunks[c][r] + counts[t][r]; keys go to their
+//                      slots in index order (stable).
 //
-// The order inside a bucket is the original key order (stable), so the
-// output is deterministic.  Digests are recomputed in the scatter pass
-// instead of being stored between passes (hashing costs less than a round
-// trip of 8 B per key through HBM).
+// Scatter kernels:
+//   _staged  (8/16/32-B keys, nranks <= 2048; default) sorts the tile by bucket
+//            in LDS first and then writes each bucket's run of the tile with
+//            consecutive lanes, so stores are coalesced runs, not 64 scattered
+//            8-byte pieces per instruction; tiles are dealt to XCDs in
+//            contiguous ranges so that the runs of neighbouring tiles meet in
+//            the same L2 and leave it as whole lines.
+//   _reg     (8/16/32-B keys, larger nranks) scatters straight from VGPRs.
+//   _wg      (any key length) re-reads keys from L2 in the scatter pass.
+// Lanes holding the same bucket find each other with ceil(log2 nranks)
+// ballots; the group leader advances the bucket's slot in LDS.
 #pragma once
 
 #include "kernels.h"
 
 namespace pdht {
 
-constexpr u64 kBucketTile = 4096;      // keys per tile
+constexpr u64 kBucketMinTile = 2048;   // smallest tile of any scatter kernel (workspace sizing)
 constexpr u32 kBucketMaxRanks = 8192;  // LDS bins (32 KiB)
+constexpr u32 kBucketChunk = 32;       // tiles per colscan chunk
+constexpr u32 kStagedMaxRanks = 2048;
 
 __device__ __forceinline__ u64 packed_key_hash(const uint8_t *keys, u64 i, u32 L) {
   return city64(GlobalReader{keys + i * (u64)L}, (u64)L);
 }
 
+// First slot of tile t in bucket r (after the scans).
+struct TileStarts {
+  const u32 *counts;  // [ntiles][nranks], exclusive prefix within the chunk
+  const u32 *chunks;  // [nchunks][nranks], exclusive prefix over chunks
+  const u64 *base;    // [nranks], exclusive prefix over buckets
+  u32 nranks;
+  __device__ __forceinline__ u32 at(u32 r, u64 t) const {
+    return (u32)(base[r] + chunks[(t / kBucketChunk) * nranks + r] + counts[t * nranks + r]);
+  }
+};
+
+// XCD-contiguous tile order: workgroup b runs on XCD b % 8 (round-robin
+// dispatch), so XCD x is given tiles [x*ntiles/8, (x+1)*ntiles/8) and its
+// workgroups walk them in lockstep.
+struct TileOrder {
+  u64 t, end, step;
+  __device__ __forceinline__ TileOrder(u64 ntiles) {
+    if (gridDim.x >= 8 && gridDim.x % 8 == 0) {
+      const u64 x = blockIdx.x % 8, per = gridDim.x / 8;
+      t = x * ntiles / 8 + blockIdx.x / 8;
+      end = (x + 1) * ntiles / 8;
+      step = per;
+    } else {
+      t = blockIdx.x;
+      end = ntiles;
+      step = gridDim.x;
+    }
+  }
+};
+
+// ------------------------------------------------------------- counting ---
 __global__ __launch_bounds__(kBlock) void k_bucket_count(const uint8_t *__restrict__ keys, u32 L,
                                                          u64 n, FastMod rk, u32 nranks,
-                                                         u32 *__restrict__ counts, u64 ntiles) {
+                                                         u32 *__restrict__ counts, u64 ntiles,
+                                                         u64 tile) {
   extern __shared__ u32 hist[];  // nranks bins
   for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
     for (u32 r = threadIdx.x; r < nranks; r += kBlock) hist[r] = 0;
     __syncthreads();
-    const u64 k0 = t * kBucketTile;
-    const u64 kend = (k0 + kBucketTile < n) ? k0 + kBucketTile : n;
+    const u64 k0 = t * tile;
+    const u64 kend = (k0 + tile < n) ? k0 + tile : n;
+#pragma unroll 4
     for (u64 i = k0 + threadIdx.x; i < kend; i += kBlock)
       atomicAdd(&hist[(u32)rk.mod(packed_key_hash(keys, i, L))], 1u);
     __syncthreads();
-    for (u32 r = threadIdx.x; r < nranks; r += kBlock) counts[(u64)r * ntiles + t] = hist[r];
+    for (u32 r = threadIdx.x; r < nranks; r += kBlock) counts[t * nranks + r] = hist[r];
     __syncthreads();
   }
 }
 
-// One workgroup per rank: exclusive scan of counts[rank][0..ntiles) in place,
-// the rank's total to totals[rank].
-__global__ __launch_bounds__(kBlock) void k_bucket_scan(u32 *__restrict__ counts, u64 ntiles,
-                                                        u64 *__restrict__ totals) {
-  __shared__ u64 part[kBlock];
-  u32 *row = counts + (u64)blockIdx.x * ntiles;
-  const u64 per = (ntiles + kBlock - 1) / kBlock;
-  const u64 lo = threadIdx.x * per;
-  const u64 hi = (lo + per < ntiles) ? lo + per : ntiles;
-  u64 s = 0;
-  for (u64 t = lo; t < hi; ++t) s += row[t];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    u64 run = 0;
-    for (int k = 0; k < kBlock; ++k) {
-      const u64 v = part[k];
-      part[k] = run;
-      run += v;
+// Packed 8/16/32-B keys: 128 B of keys per lane loaded before any is hashed.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_bucket_count_reg(const uint8_t *__restrict__ keys, u64 n,
+                                                             FastMod rk, u32 nranks,
+                                                             u32 *__restrict__ counts, u64 ntiles,
+                                                             u64 tile) {
+  constexpr int U = 128 / L;
+  extern __shared__ u32 hist[];
+  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (u32 r = threadIdx.x; r < nranks; r += kBlock) hist[r] = 0;
+    __syncthreads();
+    const u64 k0 = t * tile;
+    const u64 kend = (k0 + tile < n) ? k0 + tile : n;
+    for (u64 i = k0 + threadIdx.x; i < kend; i += (u64)kBlock * U) {
+      RegReader<L / 4> kr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_key_regs<L, false>(keys, min(i + u * kBlock, n - 1), kr[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i + u * kBlock < kend) atomicAdd(&hist[(u32)rk.mod(city64(kr[u], (u64)L))], 1u);
     }
-    totals[blockIdx.x] = run;
+    __syncthreads();
+    for (u32 r = threadIdx.x; r < nranks; r += kBlock) counts[t * nranks + r] = hist[r];
+    __syncthreads();
   }
-  __syncthreads();
-  u64 run = part[threadIdx.x];
-  for (u64 t = lo; t < hi; ++t) {
-    const u32 v = row[t];
-    row[t] = (u32)run;
-    run += v;
+}
+
+// ---------------------------------------------------------------- scans ---
+// One wave per (64 ranks, chunk): lane = rank.  The chunk's rows are loaded
+// before any is written back (a load wait would also wait for the stores).
+__global__ __launch_bounds__(64) void k_bucket_colscan(u32 *__restrict__ counts, u64 ntiles,
+                                                       u32 nranks, u32 *__restrict__ chunks) {
+  const u32 r = blockIdx.x * 64 + threadIdx.x;
+  const u64 t0 = (u64)blockIdx.y * kBucketChunk;
+  if (r >= nranks) return;
+  u32 v[kBucketChunk];
+#pragma unroll
+  for (u32 j = 0; j < kBucketChunk; ++j) v[j] = t0 + j < ntiles ? counts[(t0 + j) * nranks + r] : 0;
+  u32 run = 0;
+#pragma unroll
+  for (u32 j = 0; j < kBucketChunk; ++j) {
+    if (t0 + j < ntiles) counts[(t0 + j) * nranks + r] = run;
+    run += v[j];
   }
+  chunks[(u64)blockIdx.y * nranks + r] = run;
+}
+
+// Thread = rank: exclusive scan over the chunk sums (in place) and the total.
+__global__ __launch_bounds__(kBlock) void k_bucket_chunkscan(u32 *__restrict__ chunks, u64 nchunks,
+                                                             u32 nranks, u64 *__restrict__ totals) {
+  const u32 r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= nranks) return;
+  constexpr u32 B = 16;
+  u64 run = 0;
+  for (u64 c0 = 0; c0 < nchunks; c0 += B) {
+    u32 v[B];
+#pragma unroll
+    for (u32 j = 0; j < B; ++j) v[j] = c0 + j < nchunks ? chunks[(c0 + j) * nranks + r] : 0;
+#pragma unroll
+    for (u32 j = 0; j < B; ++j) {
+      if (c0 + j < nchunks) chunks[(c0 + j) * nranks + r] = (u32)run;
+      run += v[j];
+    }
+  }
+  totals[r] = run;
 }
 
 // Exclusive scan of the per-rank totals (one workgroup) -> bucket offsets.
@@ -111,6 +188,241 @@ __global__ __launch_bounds__(kBlock) void k_bucket_base(const u64 *__restrict__ 
   }
 }
 
+// ------------------------------------------------------------- helpers ---
+// Lanes whose r equals mine (AND of per-bit ballots; invalid lanes excluded).
+__device__ __forceinline__ u64 same_bucket_lanes(bool valid, u32 r, u32 nbits) {
+  u64 same = __ballot(valid);
+  for (u32 b = 0; b < nbits; ++b) {
+    const u64 m = __ballot(valid && ((r >> b) & 1u));
+    same &= ((r >> b) & 1u) ? m : ~m;
+  }
+  return same;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Exclusive scan of one value per thread over an NW-wave workgroup.
+template <int NW>
+__device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW words */) {
+  const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  u32 x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 y = __shfl_up(x, d);
+    if (lane >= (u32)d) x += y;
+  }
+  if (lane == 63) scratch[wave] = x;
+  __syncthreads();
+  u32 off = 0;
+#pragma unroll
+  for (u32 w = 0; w < (u32)NW; ++w)
+    if (w < wave) off += scratch[w];
+  __syncthreads();
+  return off + x - v;
+}
+
+template <int L>
+__device__ __forceinline__ void store_key_row(uint8_t *dst, const RegReader<L / 4> &k) {
+  if constexpr (L == 8) {
+    typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u32x2 *>(dst) = u32x2{k.d[0], k.d[1]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < L / 16; ++j)
+      reinterpret_cast<u32x4 *>(dst)[j] = u32x4{k.d[4 * j], k.d[4 * j + 1], k.d[4 * j + 2], k.d[4 * j + 3]};
+  }
+}
+
+// ------------------------------------------------------ staged scatter ---
+// Tile = 4 waves x 16 groups x 64 lanes = 4096 keys; wave w owns the
+// contiguous quarter [w*1024, (w+1)*1024).
+//   A: load + hash the wave's keys into VGPRs, count them into run[w][r];
+//   B: tile-local bucket starts ls[r] (block scan); run[w][r] = ls[r] + keys of
+//      bucket r in waves < w; delta[r] = (global start of the tile's run) - ls[r];
+//   C: each key's tile-local sorted slot lp (ballot rank within the group,
+//      leader advances run[w][r]); digest and tile offset staged at lp;
+//   D: thread j takes staged entry j -> global slot delta[r] + j: mbits,
+//      ptindex and index stores are runs of consecutive lanes;
+//   E: the keys, 8 bytes at a time, through the same staging buffer.
+// Shapes tried (r01, tools/gpu_session.sh bench_bucket@v): 8x16 and 8x8 tiles,
+// 4x8, slots of D kept in LDS, tile starts prefetched with the keys -- all
+// 8-45 % slower than this one on 16M x 8-B keys, 1024 ranks.
+constexpr int kStW = 4, kStKPL = 16;
+constexpr u32 kStTile = kStW * kStKPL * 64;
+constexpr size_t staged_lds_bytes(u32 nranks) {
+  return (size_t)kStTile * 8 + (size_t)kStTile * 2 + (size_t)kStW * nranks * 4 + (size_t)nranks * 4;
+}
+template <int L>
+__global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
+    const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
+    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
+    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out) {
+  extern __shared__ u64 lds64[];
+  u64 *stage = lds64;                                              // [kStTile]
+  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kStTile);  // [kStTile]
+  u32 *run = reinterpret_cast<u32 *>(sidx + kStTile);              // [kStW][nranks]
+  u32 *delta = run + kStW * nranks;                                // [nranks]
+  __shared__ u32 scan_scratch[kStW];
+  constexpr u32 kSub = kStKPL * 64;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1;
+  u32 *myrun = run + wave * nranks;
+  const u32 per = (nranks + kBlock - 1) / kBlock;
+  const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
+  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
+    const u64 t = o.t;
+    const u64 tbase = t * kStTile;
+    const u32 tn = (u32)min((u64)kStTile, n - tbase);
+    for (u32 j = threadIdx.x; j < kStW * nranks; j += kBlock) run[j] = 0;
+    const u32 q0 = wave * kSub + lane;
+    RegReader<L / 4> kr[kStKPL];
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g) load_key_regs<L, true>(keys, min(tbase + q0 + g * 64, n - 1), kr[g]);
+    u64 h[kStKPL];
+    u32 rr[kStKPL];
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g) {
+      h[g] = city64(kr[g], (u64)L);
+      rr[g] = (u32)rk.mod(h[g]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g)
+      if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
+    __syncthreads();
+    u32 s = 0;
+    for (u32 r = rb0; r < rb1; ++r)
+#pragma unroll
+      for (int w = 0; w < kStW; ++w) s += run[w * nranks + r];
+    u32 acc = block_exclusive_scan<kStW>(s, scan_scratch);
+    for (u32 r = rb0; r < rb1; ++r) {
+      delta[r] = ts.at(r, t) - acc;
+#pragma unroll
+      for (int w = 0; w < kStW; ++w) {
+        const u32 v = run[w * nranks + r];
+        run[w * nranks + r] = acc;
+        acc += v;
+      }
+    }
+    __syncthreads();
+    u32 lp[kStKPL];
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g) {
+      const bool valid = q0 + g * 64 < tn;
+      const u64 same = same_bucket_lanes(valid, rr[g], nbits);
+      const u32 ahead = (u32)__builtin_popcountll(same & below);
+      lp[g] = valid ? myrun[rr[g]] + ahead : 0;
+      wave_lds_sync();
+      if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
+      if (valid) {
+        stage[lp[g]] = h[g];
+        sidx[lp[g]] = (uint16_t)(q0 + g * 64);
+      }
+      wave_lds_sync();
+    }
+    __syncthreads();
+    constexpr int kPer = kStTile / kBlock;
+    u32 gp[kPer];
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 j = jj * kBlock + threadIdx.x;
+      if (j < tn) {
+        const u64 hv = stage[j];
+        gp[jj] = delta[(u32)rk.mod(hv)] + j;
+        mbits_out[gp[jj]] = hv;
+        if (ptindex_out) ptindex_out[gp[jj]] = (u32)pt.mod(hv);
+        if (index_out) index_out[gp[jj]] = tbase + sidx[j];
+      }
+    }
+    if (keys_out) {
+#pragma unroll
+      for (int c = 0; c < L / 8; ++c) {
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < kStKPL; ++g)
+          if (q0 + g * 64 < tn)
+            stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < kPer; ++jj) {
+          const u32 j = jj * kBlock + threadIdx.x;
+          if (j < tn) *reinterpret_cast<u64 *>(keys_out + (u64)gp[jj] * L + c * 8) = stage[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------- register scatter (no staging) ---
+// Tile = W waves x KPL groups; keys, digests and ranks stay in VGPRs, so the
+// scatter pass issues no loads: on CDNA a load wait is a vmcnt wait, which
+// also counts the scattered stores already in flight.
+template <int W, int L, int KPL>
+__global__ __launch_bounds__(W * 64) void k_bucket_scatter_reg(
+    const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
+    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
+    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out) {
+  extern __shared__ u32 run[];  // [W][nranks]
+  constexpr u64 kSub = (u64)KPL * 64, kTile = W * kSub;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1;
+  u32 *myrun = run + wave * nranks;
+  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
+    const u64 t = o.t;
+    for (u32 j = threadIdx.x; j < W * nranks; j += W * 64) run[j] = 0;
+    const u64 k0 = t * kTile + wave * kSub + lane;
+    RegReader<L / 4> kr[KPL];
+#pragma unroll
+    for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(k0 + (u64)g * 64, n - 1), kr[g]);
+    u64 h[KPL];
+    u32 rr[KPL];
+#pragma unroll
+    for (int g = 0; g < KPL; ++g) {
+      h[g] = city64(kr[g], (u64)L);
+      rr[g] = (u32)rk.mod(h[g]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < KPL; ++g)
+      if (k0 + (u64)g * 64 < n) atomicAdd(&myrun[rr[g]], 1u);
+    __syncthreads();
+    for (u32 r = threadIdx.x; r < nranks; r += W * 64) {
+      u32 acc = ts.at(r, t);
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const u32 v = run[w * nranks + r];
+        run[w * nranks + r] = acc;
+        acc += v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < KPL; ++g) {
+      const u64 i = k0 + (u64)g * 64;
+      const bool valid = i < n;
+      const u64 same = same_bucket_lanes(valid, rr[g], nbits);
+      const u32 ahead = (u32)__builtin_popcountll(same & below);
+      const u32 pos = valid ? myrun[rr[g]] + ahead : 0;
+      wave_lds_sync();
+      if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
+      if (valid) {
+        mbits_out[pos] = h[g];
+        if (ptindex_out) ptindex_out[pos] = (u32)pt.mod(h[g]);
+        if (index_out) index_out[pos] = i;
+        if (keys_out) store_key_row<L>(keys_out + (u64)pos * L, kr[g]);
+      }
+      wave_lds_sync();
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------- generic-length scatter ---
 // Copy one L-byte key row (dword pieces when both rows are 4-B aligned).
 __device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L) {
   if ((((uintptr_t)dst | (uintptr_t)src | L) & 3) == 0) {
@@ -122,56 +434,61 @@ __device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L
   }
 }
 
-// One wave per workgroup; tile t's keys are visited in index order, 64 at a
-// time.  run[r] = next free slot of bucket r for this tile (global position).
-__global__ __launch_bounds__(64) void k_bucket_scatter(
+// Tile = W waves x 32 groups; wave w owns a contiguous 2048-key sub-range.
+// Counting pass hashes; the scatter pass hashes again from L2-resident keys
+// (32 unrolled generic-length hashes per lane do not fit in VGPRs).
+constexpr int kScatKPL = 32;
+template <int W>
+__global__ __launch_bounds__(W * 64) void k_bucket_scatter_wg(
     const uint8_t *__restrict__ keys, u32 L, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
-    const u32 *__restrict__ counts, const u64 *__restrict__ base, u64 ntiles,
-    uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out, u32 *__restrict__ ptindex_out,
-    u64 *__restrict__ index_out) {
-  extern __shared__ u32 run[];  // nranks
-  const u32 lane = threadIdx.x;
+    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
+    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out) {
+  extern __shared__ u32 run[];  // [W][nranks]
+  constexpr u64 kSub = (u64)kScatKPL * 64, kTile = W * kSub;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u64 below = (1ull << lane) - 1;
-  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    for (u32 r = lane; r < nranks; r += 64) run[r] = (u32)(base[r] + counts[(u64)r * ntiles + t]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const u64 k0 = t * kBucketTile;
-    const u64 kend = (k0 + kBucketTile < n) ? k0 + kBucketTile : n;
-    for (u64 g = k0; g < kend; g += 64) {
-      const u64 i = g + lane;
-      const bool valid = i < kend;
-      u64 h = 0;
-      u32 r = 0;
-      if (valid) {
-        h = packed_key_hash(keys, i, L);
-        r = (u32)rk.mod(h);
+  u32 *myrun = run + wave * nranks;
+  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
+    const u64 t = o.t;
+    for (u32 j = threadIdx.x; j < W * nranks; j += W * 64) run[j] = 0;
+    __syncthreads();
+    const u64 k0 = t * kTile + wave * kSub + lane;
+#pragma unroll 4
+    for (int g = 0; g < kScatKPL; ++g) {
+      const u64 i = k0 + (u64)g * 64;
+      if (i < n) atomicAdd(&myrun[(u32)rk.mod(packed_key_hash(keys, i, L))], 1u);
+    }
+    __syncthreads();
+    for (u32 r = threadIdx.x; r < nranks; r += W * 64) {
+      u32 acc = ts.at(r, t);
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const u32 v = run[w * nranks + r];
+        run[w * nranks + r] = acc;
+        acc += v;
       }
-      // lanes holding the same rank: AND of per-bit ballots
-      u64 same = __ballot(valid);
-      for (u32 b = 0; b < nbits; ++b) {
-        const u64 m = __ballot(valid && ((r >> b) & 1u));
-        same &= ((r >> b) & 1u) ? m : ~m;
-      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int g = 0; g < kScatKPL; ++g) {
+      const u64 i = k0 + (u64)g * 64;
+      const bool valid = i < n;
+      const u64 h = valid ? packed_key_hash(keys, i, L) : 0;
+      const u32 r = (u32)rk.mod(h);
+      const u64 same = same_bucket_lanes(valid, r, nbits);
       const u32 ahead = (u32)__builtin_popcountll(same & below);
-      const u32 size = (u32)__builtin_popcountll(same);
-      u32 pos = 0;
-      if (valid) pos = run[r] + ahead;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // every lane has read run[] before it moves
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (valid && ahead == 0) run[r] += size;
+      const u32 pos = valid ? myrun[r] + ahead : 0;
+      wave_lds_sync();
+      if (valid && ahead == 0) myrun[r] += (u32)__builtin_popcountll(same);
       if (valid) {
         mbits_out[pos] = h;
         if (ptindex_out) ptindex_out[pos] = (u32)pt.mod(h);
         if (index_out) index_out[pos] = i;
         if (keys_out) copy_row(keys_out + (u64)pos * L, keys + i * (u64)L, L);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_lds_sync();
     }
+    __syncthreads();
   }
 }
 

@@ -196,8 +196,6 @@ struct FastMod {
 };
 
 constexpr u32 kHistLds = 4096;  // per-workgroup LDS bins before going global
-constexpr u32 kHistPartHdr = 64;  // u32 words before the partial rows (word 0 = rows written)
-constexpr u32 kHistRedRows = 64;  // partial rows folded per k_hist_reduce thread
 
 // pdht_hash placement (libpdht/hash.c:26-29) + rankputs histogram
 // (putget.c:55).
@@ -212,8 +210,6 @@ struct SinkPlaceT {
   u64 *hist;
   FastMod pt, rk;
   u32 nranks;
-  u32 *part;     // per-workgroup partial rows (k_hist_reduce), or NULL
-  u32 part_cap;  // rows available in `part`
   __device__ __forceinline__ void init() {
     if (hist && nranks <= kHistLds) {
       for (u32 r = threadIdx.x; r < nranks; r += blockDim.x) lds_hist[r] = 0;
@@ -237,40 +233,19 @@ struct SinkPlaceT {
   __device__ __forceinline__ void flush() {
     if (hist && nranks <= kHistLds) {
       __syncthreads();
-      if (part && blockIdx.x < part_cap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) part[0] = gridDim.x;
-        u32 *row = part + kHistPartHdr + (u64)blockIdx.x * nranks;
-        for (u32 r = threadIdx.x; r < nranks; r += blockDim.x) row[r] = lds_hist[r];
-      } else {
-        for (u32 r = threadIdx.x; r < nranks; r += blockDim.x)
-          if (lds_hist[r]) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)lds_hist[r]);
-      }
+      // one device-scope atomic per bin per workgroup (a two-level variant,
+      // partial rows + a reduce kernel, measured no faster: r01 placebench)
+      for (u32 r = threadIdx.x; r < nranks; r += blockDim.x)
+        if (lds_hist[r]) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)lds_hist[r]);
     }
   }
 };
-
-// Folds the partial rows of the first min(gridDim of the placement launch,
-// cap) workgroups into hist: thread = bin, blockIdx.y = a run of rows.
-__global__ __launch_bounds__(kBlock) void k_hist_reduce(const u32 *__restrict__ part, u32 cap,
-                                                        u32 nranks, u64 *__restrict__ hist) {
-  const u32 rows = min(part[0], cap);
-  const u32 r = blockIdx.x * kBlock + threadIdx.x;
-  const u32 b0 = blockIdx.y * kHistRedRows;
-  if (r >= nranks || b0 >= rows) return;
-  const u32 b1 = min(rows, b0 + kHistRedRows);
-  const u32 *p = part + kHistPartHdr + (u64)b0 * nranks + r;
-  u64 sum = 0;
-#pragma unroll 16
-  for (u32 b = b0; b < b1; ++b, p += nranks) sum += *p;
-  if (sum) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)sum);
-}
 typedef SinkPlaceT<false> SinkPlace;
 template <>
 struct NtSink<SinkPlace> {
   typedef SinkPlaceT<true> type;
   static __host__ type make(SinkPlace s) {
-    return type{s.lds_hist, s.mbits, s.ptindex, s.rank, s.rank_stride, s.hist, s.pt, s.rk, s.nranks,
-                s.part, s.part_cap};
+    return type{s.lds_hist, s.mbits, s.ptindex, s.rank, s.rank_stride, s.hist, s.pt, s.rk, s.nranks};
   }
 };
 
@@ -317,9 +292,10 @@ __global__ __launch_bounds__(kBlock) void k_fixed_direct(const uint8_t *__restri
   const u64 stride = (u64)gridDim.x * kBlock;
   for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride * U) {
     RegReader<L / 4> r[U];
+    // unconditional (clamped) loads: a load under a lane-divergent branch is
+    // followed by its own vmcnt(0), which would serialise the U keys
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (i + u * stride < n) load_key_regs<L, NT>(keys, i + u * stride, r[u]);
+    for (int u = 0; u < U; ++u) load_key_regs<L, NT>(keys, min(i + u * stride, n - 1), r[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (i + u * stride < n) sink.put(i + u * stride, algo(r[u], (u64)L));

@@ -50,12 +50,6 @@ static int current_device(int *dev) {
   DevInfo &d = g_dev[*dev];
   std::call_once(d.once, [&] {
     d.err = hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, *dev);
-    // stream-ordered scratch (histogram partials) stays cached in the pool
-    hipMemPool_t pool;
-    if (d.err == hipSuccess && hipDeviceGetDefaultMemPool(&pool, *dev) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
   });
   if (d.err != hipSuccess) return fail("%s (querying CU count)", hipGetErrorString(d.err));
   return 0;
@@ -534,31 +528,8 @@ PDHT_API int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n, ui
                                   uint32_t nranks, uint64_t *mbits, uint32_t *ptindex, void *rank,
                                   size_t rank_stride, uint64_t *hist, pdht_hip_stream_t s) {
   if (int rc = check_place(n, mbits, nptes, nranks, rank, rank_stride)) return rc;
-  SinkPlace sink = make_place_sink(mbits, ptindex, rank, rank_stride, hist, nptes, nranks);
-  if (!hist || nranks > kHistLds || n == 0 || g_variant.load(std::memory_order_relaxed) == 19)
-    return launch_fixed(keys, keysize, keysize, n, AlgoCity64{}, sink, ST(s));
-  // Two-level rankputs histogram: each workgroup stores its LDS counts as a
-  // partial row; k_hist_reduce folds the rows into `hist` with one atomic per
-  // bin per 64 rows.  A global atomic per bin per workgroup (variant 19) puts
-  // thousands of same-address device-scope atomics on every bin at the end of
-  // the launch.
-  int dev;
-  if (int rc = current_device(&dev)) return rc;
-  const u32 cap = (u32)std::max(1, g_dev[dev].cus) * (u32)std::max(16, env_int("PDHT_HIP_BLOCKS_PER_CU", 0));
-  const size_t bytes = ((size_t)kHistPartHdr + (size_t)cap * nranks) * sizeof(u32);
-  void *part = nullptr;
-  HIP_TRY(hipMallocAsync(&part, bytes, ST(s)));
-  sink.part = static_cast<u32 *>(part);
-  sink.part_cap = cap;
-  int rc = launch_fixed(keys, keysize, keysize, n, AlgoCity64{}, sink, ST(s));
-  if (rc == 0) {
-    const dim3 grid((nranks + kBlock - 1) / kBlock, (cap + kHistRedRows - 1) / kHistRedRows);
-    k_hist_reduce<<<grid, kBlock, 0, ST(s)>>>(sink.part, cap, nranks, hist);
-    if (hipGetLastError() != hipSuccess) rc = fail("k_hist_reduce launch failed%s", "");
-  }
-  const hipError_t e = hipFreeAsync(part, ST(s));
-  if (rc == 0 && e != hipSuccess) return fail("%s (hipFreeAsync)", hipGetErrorString(e));
-  return rc;
+  return launch_fixed(keys, keysize, keysize, n, AlgoCity64{},
+                      make_place_sink(mbits, ptindex, rank, rank_stride, hist, nptes, nranks), ST(s));
 }
 
 // -------------------------------------------------------- host batches ---
@@ -762,18 +733,22 @@ PDHT_API int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
 // ------------------------------------------------- destination bucketing ---
 namespace pdht {
 struct BucketWs {
-  u32 *counts;
+  u32 *counts, *chunks;
   u64 *totals, *base;
   size_t bytes;
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
+// Sized for the smallest tile any scatter kernel uses.
 static BucketWs bucket_layout(void *ws, size_t n, u32 nranks) {
-  const u64 ntiles = (n + kBucketTile - 1) / kBucketTile;
+  const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
+  const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   BucketWs w{};
   uint8_t *p = static_cast<uint8_t *>(ws);
   size_t off = 0;
   w.counts = reinterpret_cast<u32 *>(p + off);
   off += round256((size_t)nranks * ntiles * 4);
+  w.chunks = reinterpret_cast<u32 *>(p + off);
+  off += round256((size_t)nranks * nchunks * 4);
   w.totals = reinterpret_cast<u64 *>(p + off);
   off += round256((size_t)nranks * 8);
   w.base = reinterpret_cast<u64 *>(p + off);
@@ -781,6 +756,63 @@ static BucketWs bucket_layout(void *ws, size_t n, u32 nranks) {
   w.bytes = off;
   return w;
 }
+
+static int set_lds(const void *fn, size_t bytes) {
+  if (bytes > 65536)
+    HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return 0;
+}
+
+struct BucketArgs {
+  const uint8_t *k;
+  u64 n;
+  FastMod pt, rk;
+  u32 nranks, nbits;
+  TileStarts ts;
+  u64 ntiles;
+  uint8_t *ko;
+  u64 *mb;
+  u32 *pi;
+  u64 *ix;
+};
+
+template <int L>
+static int launch_staged(const BucketArgs &a, hipStream_t st, int dev) {
+  static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
+                                       "k_bucket_scatter_staged<32B>"};
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = staged_lds_bytes(a.nranks);
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_staged<L>), bytes)) return rc;
+  unsigned g = grid_for(a.ntiles, bytes <= 80 * 1024 ? 2 : 1, dev);
+  if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
+  k_bucket_scatter_staged<L><<<g, kBlock, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts,
+                                                      a.ntiles, a.ko, a.mb, a.pi, a.ix);
+  return 0;
+}
+
+template <int W, int L, int KPL>
+static int launch_reg(const BucketArgs &a, hipStream_t st, int dev) {
+  static const char *const names[3] = {"k_bucket_scatter_reg<8B>", "k_bucket_scatter_reg<16B>",
+                                       "k_bucket_scatter_reg<32B>"};
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = (size_t)W * a.nranks * 4;
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_reg<W, L, KPL>), bytes)) return rc;
+  k_bucket_scatter_reg<W, L, KPL><<<grid_for(a.ntiles, 2, dev), W * 64, bytes, st>>>(
+      a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi, a.ix);
+  return 0;
+}
+
+template <int W>
+static int launch_wg(const BucketArgs &a, u32 L, hipStream_t st, int dev) {
+  g_kernel = W == 8 ? "k_bucket_scatter_wg<8>" : "k_bucket_scatter_wg<4>";
+  const size_t bytes = (size_t)W * a.nranks * 4;
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_wg<W>), bytes)) return rc;
+  k_bucket_scatter_wg<W><<<grid_for(a.ntiles, 4, dev), W * 64, bytes, st>>>(
+      a.k, L, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi, a.ix);
+  return 0;
+}
+
+enum class BucketKernel { kStaged, kReg, kGeneric };
 }  // namespace pdht
 
 PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
@@ -802,25 +834,70 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
   int dev;
   if (int rc = current_device(&dev)) return rc;
   hipStream_t st = ST(s);
-  const u64 ntiles = (n + kBucketTile - 1) / kBucketTile;
-  const FastMod pt = make_fastmod(nptes), rk = make_fastmod(nranks);
-  u32 nbits = 0;
-  while ((1u << nbits) < nranks) ++nbits;
-  const uint8_t *k = static_cast<const uint8_t *>(keys);
-  const size_t lds = (size_t)nranks * 4;
-  g_kernel = "k_bucket";
+  // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter up to
+  // 2048 ranks, register scatter above; other lengths -> generic.  Variants:
+  // 21 forces generic, 22 forces register.
+  const int variant = g_variant.load(std::memory_order_relaxed);
+  const uintptr_t al = (uintptr_t)keys | (uintptr_t)keys_out;
+  const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
+  BucketKernel kind = !fixed || variant == 21        ? BucketKernel::kGeneric
+                      : variant == 22 || nranks > kStagedMaxRanks ? BucketKernel::kReg
+                                                               : BucketKernel::kStaged;
+  const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
+  const int reg_kpl = keysize == 32 ? 8 : 16;
+  const u64 tile = kind == BucketKernel::kStaged ? kStTile
+                   : kind == BucketKernel::kReg  ? (u64)waves * reg_kpl * 64
+                                                 : (u64)waves * kScatKPL * 64;
+  const u64 ntiles = (n + tile - 1) / tile;
+  const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
+  BucketArgs a{};
+  a.k = static_cast<const uint8_t *>(keys);
+  a.n = n;
+  a.pt = make_fastmod(nptes);
+  a.rk = make_fastmod(nranks);
+  a.nranks = nranks;
+  while ((1u << a.nbits) < nranks) ++a.nbits;
+  a.ts = TileStarts{w.counts, w.chunks, w.base, nranks};
+  a.ntiles = ntiles;
+  a.ko = static_cast<uint8_t *>(keys_out);
+  a.mb = mbits_out;
+  a.pi = ptindex_out;
+  a.ix = index_out;
+  const size_t hist_lds = (size_t)nranks * 4;
   if (ntiles) {
-    k_bucket_count<<<grid_for(ntiles, 8, dev), kBlock, lds, st>>>(k, (u32)keysize, n, rk, nranks,
-                                                                  w.counts, ntiles);
-    k_bucket_scan<<<nranks, kBlock, 0, st>>>(w.counts, ntiles, w.totals);
+    const unsigned gc = grid_for(ntiles, 8, dev);
+    if (fixed && keysize == 8)
+      k_bucket_count_reg<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
+    else if (fixed && keysize == 16)
+      k_bucket_count_reg<16><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
+    else if (fixed && keysize == 32)
+      k_bucket_count_reg<32><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
+    else
+      k_bucket_count<<<gc, kBlock, hist_lds, st>>>(a.k, (u32)keysize, n, a.rk, nranks, w.counts, ntiles,
+                                                   tile);
+    k_bucket_colscan<<<dim3((nranks + 63) / 64, (unsigned)nchunks), 64, 0, st>>>(w.counts, ntiles, nranks,
+                                                                                 w.chunks);
+    k_bucket_chunkscan<<<(nranks + kBlock - 1) / kBlock, kBlock, 0, st>>>(w.chunks, nchunks, nranks,
+                                                                        w.totals);
   } else {
     HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
   }
   k_bucket_base<<<1, kBlock, 0, st>>>(w.totals, nranks, w.base, bucket_offsets);
-  if (ntiles)
-    k_bucket_scatter<<<grid_for(ntiles, 16, dev), 64, lds, st>>>(
-        k, (u32)keysize, n, pt, rk, nranks, nbits, w.counts, w.base, ntiles,
-        static_cast<uint8_t *>(keys_out), mbits_out, ptindex_out, index_out);
+  g_kernel = "k_bucket_base";
+  if (ntiles) {
+    int rc = 0;
+    if (kind == BucketKernel::kStaged)
+      rc = keysize == 8    ? launch_staged<8>(a, st, dev)
+           : keysize == 16 ? launch_staged<16>(a, st, dev)
+                           : launch_staged<32>(a, st, dev);
+    else if (kind == BucketKernel::kReg)
+      rc = keysize == 8    ? (waves == 8 ? launch_reg<8, 8, 16>(a, st, dev) : launch_reg<4, 8, 16>(a, st, dev))
+           : keysize == 16 ? (waves == 8 ? launch_reg<8, 16, 16>(a, st, dev) : launch_reg<4, 16, 16>(a, st, dev))
+                           : (waves == 8 ? launch_reg<8, 32, 8>(a, st, dev) : launch_reg<4, 32, 8>(a, st, dev));
+    else
+      rc = waves == 8 ? launch_wg<8>(a, (u32)keysize, st, dev) : launch_wg<4>(a, (u32)keysize, st, dev);
+    if (rc) return rc;
+  }
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -247,7 +247,7 @@ def test_place_batch(dev, oracle, L, nptes, nranks):
 
 
 @pytest.mark.parametrize("L", [8, 64])
-@pytest.mark.parametrize("variant", [0, 19])  # 0: two-level histogram, 19: per-workgroup atomics
+@pytest.mark.parametrize("variant", [0, 16, 18])
 def test_place_hist_many_workgroups(dev, oracle, L, variant):
     # enough keys for a full persistent grid; hist accumulates across calls
     rng = np.random.default_rng(L + 5)
@@ -285,13 +285,31 @@ def test_small_key_variants(dev, oracle, L, variant):
     assert (rk.cpu().numpy().view(np.uint32) == r2).all()
 
 
-@pytest.mark.parametrize("L", [8, 13, 64])
-@pytest.mark.parametrize("nranks", [1, 2, 7, 1000, 8192])
-@pytest.mark.parametrize("n", [0, 1, 4095, 100003])
-def test_bucket_batch(dev, oracle, L, nranks, n):
+BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1000, 4096, 4097, 8192)
+                for n in (0, 1, 4095, 100003)]
+BUCKET_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192)
+                 for n in (4095, 300007)]
+
+
+def _bucket_kernel(L, nranks, variant):
+    """21 forces the generic-length kernel, 22 the register (unstaged) one."""
+    if variant != 21 and L in (8, 16, 32):
+        kind = "reg" if variant == 22 or nranks > 2048 else "staged"
+        return f"k_bucket_scatter_{kind}<{L}B>"
+    return "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
+
+
+@pytest.mark.parametrize("L,nranks,n,variant", BUCKET_CASES)
+def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     rng = np.random.default_rng(L * 7 + nranks + n)
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
-    ko, mb, pt, ix, offs = P.bucket_batch(to_dev(k, dev), 3, nranks)
+    old = P.set_variant(variant)
+    try:
+        ko, mb, pt, ix, offs = P.bucket_batch(to_dev(k, dev), 3, nranks)
+        if n:
+            assert P.last_kernel() == _bucket_kernel(L, nranks, variant)
+    finally:
+        P.set_variant(old)
     m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, nranks) if n else (
         np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint32))
     order = np.argsort(r2, kind="stable")  # the reference placement, stably bucketed

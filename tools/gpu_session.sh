@@ -13,8 +13,9 @@ for step in "$@"; do
              tail -1 gpurun_out/smoke.log ;;
     bench)   timeout -k 10 240 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
              tail -1 gpurun_out/bench.log ;;
-    bench_*) cfg=${step#bench_}; timeout -k 10 300 python bench.py --config $cfg --no-cpu-baseline > gpurun_out/bench_$cfg.log 2>&1; rc=$?
-             tail -1 gpurun_out/bench_$cfg.log ;;
+    bench_*) cfg=${step#bench_}; v=${cfg#*@}; [ "$v" = "$cfg" ] && v=0; cfg=${cfg%@*}
+             timeout -k 10 300 python bench.py --config $cfg --variant $v --no-cpu-baseline > "gpurun_out/$step.log" 2>&1; rc=$?
+             tail -1 "gpurun_out/$step.log" ;;
     kbench)  timeout -k 10 300 python tools/kbench.py > gpurun_out/kbench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/kbench.log | cut -c1-200 ;;
     kbench_pc) timeout -k 10 400 python tools/kbench.py --variants 0,15 --per-cu 3,4,5 --rounds 7 > gpurun_out/kbench_pc.log 2>&1; rc=$?
@@ -25,6 +26,16 @@ for step in "$@"; do
              grep -v amdgpu.ids gpurun_out/kbench_crc.log | cut -c1-200 ;;
     prof)    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host > gpurun_out/prof.log 2>&1; rc=$?
              head -3 gpurun_out/prof/run_kernel_stats.csv | cut -c1-200 ;;
+    prof_*)  cfg=${step#prof_}; v=${cfg#*@}; [ "$v" = "$cfg" ] && v=0; cfg=${cfg%@*}; d="gpurun_out/$step"
+             timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$d" -o run --output-format csv -- python3 bench.py --config $cfg --variant $v --steps 20 --warmup 3 --no-cpu-baseline --no-host > "$d.log" 2>&1; rc=$?
+             python3 -c "import csv,sys; [print(r['Name'][:70], r['Calls'], r['AverageNs']) for r in csv.DictReader(open(sys.argv[1])) if 'pdht' in r['Name']]" "$d/run_kernel_stats.csv" ;;
+    pmc_*)   cfg=${step#pmc_}; rc=0; i=0
+             # PMCS: counter groups separated by ';' (one rocprofv3 pass each)
+             IFS=';' read -ra groups <<< "${PMCS:-FETCH_SIZE;WRITE_SIZE}"
+             for grp in "${groups[@]}"; do
+               i=$((i+1))
+               timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_${cfg}_$i" -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/pmc_${cfg}_$i.log 2>&1 || { rc=$?; break; }
+             done ;;
     pmc)     rc=0
              for ctr in FETCH_SIZE WRITE_SIZE; do
                timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$ctr" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/pmc_$ctr.log 2>&1 || { rc=$?; break; }
