@@ -150,6 +150,10 @@ int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
 int pdht_hip_set_variant(int variant);
 /* Name of the kernel the last batch call on this thread launched. */
 const char *pdht_hip_last_kernel(void);
+/* Optional: total key bytes (offsets[n] - offsets[0]) of the NEXT variable-
+ * length batch call on this thread, which then sizes its LDS window for the
+ * mean key length instead of assuming short keys.  Used by one call only. */
+int pdht_hip_set_var_bytes_hint(uint64_t total_bytes);
 /* HBM calibration: stream `bytes` (multiple of 16, 16-B aligned) through a
  * read-only kernel with 16-B coalesced loads (nt != 0: non-temporal) and
  * XOR-fold them into *out (one uint64, device).  Gives the achievable read

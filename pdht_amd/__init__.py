@@ -80,6 +80,7 @@ def _declare(L):
         "pdht_hip_version": (C.c_char_p, []),
         "pdht_hip_last_error": (C.c_char_p, []),
         "pdht_hip_last_kernel": (C.c_char_p, []),
+        "pdht_hip_set_var_bytes_hint": (C.c_int, [C.c_uint64]),
         "pdht_hip_set_variant": (C.c_int, [C.c_int]),
         "pdht_hip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
         "pdht_hip_set_device": (C.c_int, [C.c_int]),
@@ -276,6 +277,9 @@ def _check_var(data, offsets):
         raise ValueError("data must be a contiguous CUDA uint8 tensor")
     if offsets.dtype != torch.int64 or not offsets.is_cuda or not offsets.is_contiguous():
         raise ValueError("offsets must be a contiguous CUDA int64 tensor of n+1 entries")
+    # the buffer size bounds the key bytes: lets the kernel size its window
+    # for the mean key length (pdht_hip_set_var_bytes_hint, one call)
+    lib().pdht_hip_set_var_bytes_hint(data.numel())
     return offsets.numel() - 1
 
 

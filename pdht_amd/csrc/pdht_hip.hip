@@ -34,6 +34,8 @@ static int fail(const char *fmt, const char *a = "", long long b = 0) {
   } while (0)
 
 static std::atomic<int> g_variant{0};
+// Total key bytes of the next variable-length batch on this thread (0 = unknown).
+static thread_local u64 g_var_bytes_hint = 0;
 
 // ------------------------------------------------------- device state ---
 constexpr int kMaxDev = 64;
@@ -218,6 +220,8 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
 template <class Algo, class Sink>
 static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
                       Sink sink, hipStream_t st) {
+  const u64 hint = g_var_bytes_hint;
+  g_var_bytes_hint = 0;  // one call only
   if (n == 0) return 0;
   if (!bytes || !offsets) return fail("null bytes/offsets pointer%s", "");
   int dev;
@@ -253,11 +257,27 @@ static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n
         k_window_pf<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
             b, offsets, obase, 0, 0, n, algo, sink);
         break;
-      default:  // 0, 11: non-temporal window DMA + digest stores (tools/varbench.py)
+      case 11:
         g_kernel = "k_window<var,nt>";
         k_window<kWinBytes, true, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
             b, offsets, obase, 0, 0, n, algo, sink_nt);
         break;
+      default: {
+        // auto: the window that holds a wave's 64 keys at the batch's mean
+        // length (tools/varbench.py, r01): mean <= 160 B (cfg3's 16..256 mix,
+        // mean 136) -> 10224 B at 4 workgroups/CU; longer -> 16 KiB at 2.
+        // Without a byte-count hint (pdht_hip_set_var_bytes_hint) -> 10224.
+        if (hint && hint / n > 160) {
+          g_kernel = "k_window<var,nt,16K>";
+          k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
+              b, offsets, obase, 0, 0, n, algo, sink_nt);
+        } else {
+          g_kernel = "k_window<var,nt,10224>";
+          k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+              b, offsets, obase, 0, 0, n, algo, sink_nt);
+        }
+        break;
+      }
     }
   }
   HIP_TRY(hipGetLastError());
@@ -449,6 +469,10 @@ using namespace pdht;
 PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.1 (gfx950, CityHash v1.0.x)"; }
 PDHT_API const char *pdht_hip_last_error(void) { return g_err; }
 PDHT_API const char *pdht_hip_last_kernel(void) { return g_kernel; }
+PDHT_API int pdht_hip_set_var_bytes_hint(uint64_t total_bytes) {
+  g_var_bytes_hint = total_bytes;
+  return 0;
+}
 PDHT_API int pdht_hip_set_variant(int v) { return g_variant.exchange(v); }
 
 PDHT_API int pdht_hip_device_count(int *count) {
@@ -638,6 +662,7 @@ PDHT_API int pdht_city64_batch_var_host(const void *bytes, const uint64_t *offse
     if (int rc = chunk_in(s, static_cast<const uint8_t *>(bytes) + offsets[a], pin_in, 0, nbytes)) return rc;
     // offsets are always staged (tiny) so that they can be copied as-is
     HIP_TRY(hipMemcpyAsync(s.d_in + off_at, offsets + a, (cnt + 1) * 8, hipMemcpyHostToDevice, s.st));
+    g_var_bytes_hint = nbytes;
     if (int rc = launch_var(s.d_in, reinterpret_cast<const u64 *>(s.d_in + off_at), offsets[a], cnt,
                             AlgoCity64{}, Sink64{nullptr, reinterpret_cast<u64 *>(s.d_out)}, s.st))
       return rc;

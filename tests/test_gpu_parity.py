@@ -185,17 +185,23 @@ def test_var_golden_mixed(dev, golden, oracle):
     assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
 
 
-VAR_KERNELS = {0: "k_window<var,nt>", 3: "k_window<var>", 10: "k_var_sorted",
+VAR_KERNELS = {0: "auto", 3: "k_window<var>", 10: "k_var_sorted",
                11: "k_window<var,nt>", 12: "k_window<var,nt,10224>", 13: "k_window<var,nt,16K>",
                14: "k_window_pf<var>"}
+
+
+def auto_var_kernel(total_bytes, n):
+    """Variant 0's window choice (launch_var): mean key length > 160 B -> 16 KiB."""
+    return "k_window<var,nt,16K>" if total_bytes // n > 160 else "k_window<var,nt,10224>"
 
 
 @pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
 def test_var_edge_cases(dev, oracle, variant):
     old = P.set_variant(variant)
     try:
-        _var_edge_cases(dev, oracle)
-        assert P.last_kernel() == VAR_KERNELS[variant]
+        total, n = _var_edge_cases(dev, oracle)
+        want = auto_var_kernel(total, n) if variant == 0 else VAR_KERNELS[variant]
+        assert P.last_kernel() == want
     finally:
         P.set_variant(old)
 
@@ -218,12 +224,24 @@ def _var_edge_cases(dev, oracle):
         assert (u64(P.city64_var_batch(dd, od)) == oracle.city64_var(d, offs)).all()
         assert (u64(P.city128_var_batch(dd, od)) == oracle.city128_var(d, offs)).all()
         assert (u64(P.citycrc128_var_batch(dd, od)) == oracle.city128_var(d, offs, crc=True)).all()
+    return int(offs[-1]), lens.size
 
 
 def test_var_1M_mixed(dev, oracle):
     data, offs = oracle.mixed_keys(M)
     dd, od = to_dev(data, dev), to_dev(offs.astype(np.int64), dev)
     assert (u64(P.city64_var_batch(dd, od)) == oracle.city64_var(data, offs)).all()
+    assert P.last_kernel() == auto_var_kernel(data.size, M) == "k_window<var,nt,10224>"
+    # the same keys without the byte-count hint (raw C-ABI call): short-key window
+    out = torch.empty(M, dtype=torch.int64, device=dev)
+    assert P.lib().pdht_city64_batch_var_dev(dd.data_ptr(), od.data_ptr(), M, out.data_ptr(), None) == 0
+    assert P.last_kernel() == "k_window<var,nt,10224>"
+    assert (u64(out) == oracle.city64_var(data, offs)).all()
+    # long keys (mean 192 B): the 16 KiB window
+    data2, offs2 = oracle.mixed_keys(1 << 18, lo=129, hi=256)
+    got = u64(P.city64_var_batch(to_dev(data2, dev), to_dev(offs2.astype(np.int64), dev)))
+    assert P.last_kernel() == "k_window<var,nt,16K>"
+    assert (got == oracle.city64_var(data2, offs2)).all()
 
 
 # ---------------------------------------------------- fused placement ---
