@@ -17,8 +17,10 @@ Rank 0 prints one JSON line.  Besides the contract fields it carries
                    64 B key read + 8 B digest write) over its average launch
                    duration measured with HIP events on the launch stream,
                    plus HBM traffic per launch from the committed rocprofv3
-                   PMC pass (profiles/traffic_<cfg>.json) and a calibrated
-                   read-stream rate on the same buffer;
+                   PMC pass (profiles/traffic_<cfg>.json), a calibrated
+                   read-stream rate on the same buffer and (64-B configs) the
+                   kernel's own data movement with the hash replaced by an
+                   XOR fold (calibrated_key_stream_GBps);
   cpu_baseline  -- the reference city.c (oracle/_ref, or the oracle port when
                    _ref is absent) timed on this host's cores over a bounded
                    sample of the same keys (rank 0, N = 1 only);
@@ -197,6 +199,21 @@ def main():
         torch.cuda.synchronize()
         cms = float(np.median([s.elapsed_time(e) for s, e in cev]))
         calib = round(keys.numel() / (cms / 1e3) / 1e9, 1)
+    # the 64-B kernel's own data movement with the hash replaced by an XOR fold
+    calib_key = None
+    if cfg in ("cfg2", "cfg5"):
+        fold = torch.empty(n, dtype=torch.int64, device=dev)
+        P.key_stream(keys, out=fold)
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(10)]
+        for s, e in cev:
+            s.record()
+            P.key_stream(keys, out=fold)
+            e.record()
+        torch.cuda.synchronize()
+        cms = float(np.median([s.elapsed_time(e) for s, e in cev]))
+        calib_key = round(bytes_per_key * n / (cms / 1e3) / 1e9, 1)
+        del fold
 
     # ------------------------------------------------------------ parity ---
     if bucketed is not None:
@@ -229,7 +246,8 @@ def main():
                      "traffic": load_traffic(cfg, n), "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "read_only_GBps": round(total_bytes_in / (kern_ms / 1e3) / 1e9, 1),
-                     "calibrated_read_stream_GBps": calib},
+                     "calibrated_read_stream_GBps": calib,
+                     "calibrated_key_stream_GBps": calib_key},
         "parity": parity,
     }
     if rank == 0 and world == 1 and cfg in ("cfg2", "cfg4") and not a.no_host:

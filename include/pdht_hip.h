@@ -160,6 +160,11 @@ int pdht_hip_set_var_bytes_hint(uint64_t total_bytes);
  * bandwidth the hash kernels are compared with. */
 int pdht_hip_read_stream_dev(const void *buf, size_t bytes, int nt, uint64_t *out,
                              pdht_hip_stream_t stream);
+/* Key-stream calibration: n packed 64-B keys (16-B aligned) -> out[n], each
+ * digest an XOR fold of the key's bytes, moved exactly as the default 64-B
+ * CityHash64 kernel moves them (same loads, LDS transpose, stores, grid).
+ * The hash kernel's time minus this one is what the hash arithmetic costs. */
+int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out, pdht_hip_stream_t stream);
 
 #ifdef __cplusplus
 }

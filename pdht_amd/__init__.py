@@ -101,6 +101,7 @@ def _declare(L):
         "pdht_hip_splitmix64_fill_dev": (C.c_int, [_U64, _U64, _S, _V, _V]),
         "pdht_hip_mixed_lengths_dev": (C.c_int, [_U64, _U64, _S, _U32, _U32, _V, _V]),
         "pdht_hip_read_stream_dev": (C.c_int, [_V, _S, C.c_int, _V, _V]),
+        "pdht_hip_key_stream_dev": (C.c_int, [_V, _S, _V, _V]),
         "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _U32]),
         "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
         "CityHash64": (_U64, [_V, _S]),
@@ -410,6 +411,19 @@ def read_stream(buf, nt: bool = False, out=None, stream=None):
         out = torch.zeros(1, dtype=torch.int64, device=buf.device)
     _check(lib().pdht_hip_read_stream_dev(_dptr(buf), buf.numel() * buf.element_size(), int(nt),
                                           _dptr(out), _stream_ptr(stream)), "pdht_hip_read_stream_dev")
+    return out
+
+
+def key_stream(keys, out=None, stream=None):
+    """Calibration: the 64-B kernel's data movement with an XOR fold for a hash."""
+    torch = _torch()
+    n = keys.shape[0]
+    if keys.dim() != 2 or keys.shape[1] != 64 or keys.dtype != torch.uint8 or not keys.is_contiguous():
+        raise PdhtError("key_stream takes a contiguous (n, 64) uint8 tensor")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=keys.device)
+    _check(lib().pdht_hip_key_stream_dev(_dptr(keys), n, _dptr(out), _stream_ptr(stream)),
+           "pdht_hip_key_stream_dev")
     return out
 
 

@@ -127,6 +127,23 @@ struct AlgoCrc128Seed {
   }
 };
 
+// Calibration only (pdht_hip_key_stream_dev): the data movement of a hash
+// kernel with the hash replaced by an XOR fold of the key's 64 bytes.
+struct AlgoFold64 {
+  typedef u64 Out;
+  template <class R>
+  __device__ __forceinline__ Out operator()(const R &r, u64) const {
+    const Words<16> w = r.template span<64>(0);
+    u32 a = 0, b = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a ^= w.d[2 * j];
+      b ^= w.d[2 * j + 1];
+    }
+    return ((u64)b << 32) | a;
+  }
+};
+
 // ----------------------------------------------------------------- sinks ---
 // Where a digest goes.  init()/flush() run once per workgroup around the
 // grid-stride loop (every thread reaches both).

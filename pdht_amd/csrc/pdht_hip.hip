@@ -693,7 +693,8 @@ __global__ __launch_bounds__(kBlock) void k_mixed_lengths(u64 seed, u64 first, u
 
 // Read-only HBM stream (calibration), the same access shape as the hash
 // kernels: a wave owns a contiguous 4 KiB tile = 4 wave-instructions of 1 KiB
-// (16 B per lane); grid-stride over tiles; one atomic per wave.
+// (16 B per lane); grid-stride over tiles, 2 workgroups per CU (the fastest
+// read shape in tools/hbm_probe.hip: 7.0-7.2 TB/s with nt loads).
 template <bool NT>
 __global__ __launch_bounds__(kBlock) void k_read_stream(const u32x4 *__restrict__ p, u64 n16,
                                                         u64 *out) {
@@ -710,7 +711,17 @@ __global__ __launch_bounds__(kBlock) void k_read_stream(const u32x4 *__restrict_
   for (u64 i = (full << 8) + wave * 64 + lane; i < n16; i += nwaves * 64) acc ^= ld<NT>(p + i);
   u64 v = ((u64)(acc.x ^ acc.z) << 32) | (acc.y ^ acc.w);
   for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned long long *>(out), v);
+  // one atomic per workgroup: thousands of same-address atomics at the end of
+  // the stream serialise in L2 and cost ~25 % of the launch (hbm_probe.hip)
+  __shared__ u64 part[kWavesPerBlock];
+  if (lane == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 b = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) b ^= part[w];
+    atomicXor(reinterpret_cast<unsigned long long *>(out), b);
+  }
 }
 }  // namespace pdht
 
@@ -721,12 +732,30 @@ PDHT_API int pdht_hip_read_stream_dev(const void *buf, size_t bytes, int nt, uin
   int dev;
   if (int rc = current_device(&dev)) return rc;
   const u64 n16 = bytes / 16;
-  const unsigned g = grid_for(((n16 >> 8) + kWavesPerBlock) / kWavesPerBlock, 8, dev);
+  const unsigned g = grid_for(((n16 >> 8) + kWavesPerBlock) / kWavesPerBlock, 2, dev);
   const u32x4 *p = static_cast<const u32x4 *>(buf);
   if (nt)
     k_read_stream<true><<<g, kBlock, 0, ST(s)>>>(p, n16, out);
   else
     k_read_stream<false><<<g, kBlock, 0, ST(s)>>>(p, n16, out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// Key-stream calibration: exactly the default 64-B kernel's data movement
+// (k_fixed_xpose64, nt loads and stores, same grid) with the hash replaced by
+// an XOR fold, so hash cost = kernel time - this time.
+PDHT_API int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out,
+                                     pdht_hip_stream_t s) {
+  if (n == 0) return 0;
+  if (!keys || !out || ((uintptr_t)keys & 15)) return fail("bad buffer%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  Sink64T<true> sink{};
+  sink.out = out;
+  k_fixed_xpose64<AlgoFold64, Sink64T<true>, true, 2>
+      <<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, ST(s)>>>(static_cast<const uint8_t *>(keys), n,
+                                                                AlgoFold64{}, sink);
   HIP_TRY(hipGetLastError());
   return 0;
 }

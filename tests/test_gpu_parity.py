@@ -168,6 +168,17 @@ def test_read_stream_calibration_kernel(dev, nbytes):
         assert got == (int(x) << 32) | int(y)
 
 
+@pytest.mark.parametrize("n", [1, 64, 4096 * 3 + 17])
+def test_key_stream_calibration_kernel(dev, n):
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    got = u64(P.key_stream(to_dev(keys, dev)))
+    d = keys.view(np.uint32).reshape(n, 16)
+    want = (np.bitwise_xor.reduce(d[:, 1::2], axis=1).astype(np.uint64) << np.uint64(32)) | \
+        np.bitwise_xor.reduce(d[:, 0::2], axis=1).astype(np.uint64)
+    assert (got == want).all()
+
+
 def test_errors_are_loud(dev):
     k = torch.zeros((4, 8), dtype=torch.uint8, device=dev)
     with pytest.raises(P.PdhtError):
