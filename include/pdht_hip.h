@@ -165,6 +165,11 @@ int pdht_hip_read_stream_dev(const void *buf, size_t bytes, int nt, uint64_t *ou
  * CityHash64 kernel moves them (same loads, LDS transpose, stores, grid).
  * The hash kernel's time minus this one is what the hash arithmetic costs. */
 int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out, pdht_hip_stream_t stream);
+/* The same for offset-indexed keys: the variable-length kernel's window DMA,
+ * offsets reads, LDS reads of every key byte and digest stores, with the hash
+ * replaced by an XOR fold (out[i] = fold of key i; see tests). */
+int pdht_hip_key_stream_var_dev(const void *bytes, const uint64_t *offsets, size_t n, uint64_t *out,
+                                pdht_hip_stream_t stream);
 
 #ifdef __cplusplus
 }

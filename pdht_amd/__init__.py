@@ -102,6 +102,7 @@ def _declare(L):
         "pdht_hip_mixed_lengths_dev": (C.c_int, [_U64, _U64, _S, _U32, _U32, _V, _V]),
         "pdht_hip_read_stream_dev": (C.c_int, [_V, _S, C.c_int, _V, _V]),
         "pdht_hip_key_stream_dev": (C.c_int, [_V, _S, _V, _V]),
+        "pdht_hip_key_stream_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
         "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _U32]),
         "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
         "CityHash64": (_U64, [_V, _S]),
@@ -424,6 +425,15 @@ def key_stream(keys, out=None, stream=None):
         out = torch.empty(n, dtype=torch.int64, device=keys.device)
     _check(lib().pdht_hip_key_stream_dev(_dptr(keys), n, _dptr(out), _stream_ptr(stream)),
            "pdht_hip_key_stream_dev")
+    return out
+
+
+def key_stream_var(data, offsets, out=None, stream=None):
+    """Calibration: the variable-length kernel's data movement with an XOR fold."""
+    n = _check_var(data, offsets)
+    out = _out(n, 1, data.device, out)
+    _check(lib().pdht_hip_key_stream_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
+                                             _stream_ptr(stream)), "pdht_hip_key_stream_var_dev")
     return out
 
 

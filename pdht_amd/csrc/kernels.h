@@ -144,6 +144,24 @@ struct AlgoFold64 {
   }
 };
 
+// Calibration only (pdht_hip_key_stream_var_dev): every byte of a key read
+// through the same reader (16-B spans, then single bytes), XOR-folded.
+struct AlgoFoldVar {
+  typedef u64 Out;
+  template <class R>
+  __device__ __forceinline__ Out operator()(const R &r, u64 len) const {
+    u32 a = (u32)len, b = 0;
+    u32 o = 0;
+    for (; o + 16 <= len; o += 16) {
+      const Words<4> w = r.template span<16>(o);
+      a ^= w.d[0] ^ w.d[2];
+      b ^= w.d[1] ^ w.d[3];
+    }
+    for (; o < len; ++o) a ^= r.b8(o) << (8 * (o & 3));
+    return ((u64)b << 32) | a;
+  }
+};
+
 // ----------------------------------------------------------------- sinks ---
 // Where a digest goes.  init()/flush() run once per workgroup around the
 // grid-stride loop (every thread reaches both).
@@ -552,6 +570,135 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
     }
     __builtin_amdgcn_wave_barrier();  // window reused by the next tile
   }
+  sink.flush();
+}
+
+// ------------------------------------------- double-buffered window kernel ---
+// Offset-indexed keys.  k_window with two LDS windows per wave: while tile t
+// hashes out of one window, the LDS-DMA of tile t+nwaves streams into the
+// other, and the offsets of tile t+2*nwaves are already on their way.  The
+// windows are two distinct __shared__ objects and the loop is unrolled by two,
+// so every LDS read names its window and the compiler's LDS-DMA wait tracking
+// (alias scopes per LDS object) only waits for the DMA into THAT window.
+// Per tile, one vector load of offsets[k0+lane] (a key's end = its right
+// neighbour's start) and one uniform load of offsets[kend].
+template <int WIN>
+struct WinGeo {
+  u64 wlo;     // 16-B aligned window start (bytes index, relative to obase)
+  u64 start;   // this lane's key
+  u64 end;
+  u32 wbytes;  // bytes staged (<= WIN)
+};
+
+template <int WIN, class Algo, class Sink, int AUX = 2>
+__global__ __launch_bounds__(kBlock) void k_window2(const uint8_t *__restrict__ bytes,
+                                                    const u64 *__restrict__ offsets, u64 obase,
+                                                    u64 n, Algo algo, Sink sink) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  __shared__ __attribute__((aligned(16))) u32 winA[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ __attribute__((aligned(16))) u32 winB[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *const wa = winA + wave * (WIN / 4);
+  u32 *const wb = winB + wave * (WIN / 4);
+
+  // offsets of tile t: this lane's start, and the tile's end (uniform)
+  auto load_offs = [&](u64 t, u64 &a, u64 &hi) {
+    const u64 k0 = t << 6;
+    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
+    a = offsets[(k0 + lane < n) ? k0 + lane : n];
+    hi = offsets[kend];
+  };
+  auto geometry = [&](u64 a, u64 hi) {
+    WinGeo<WIN> g;
+    const u64 nb = __shfl_down(a, 1);
+    g.start = a - obase;
+    g.end = (lane == 63 ? hi : nb) - obase;
+    // readfirstlane returns int: widen through u32 (no sign extension)
+    const u64 a0 = (u64)(u32)__builtin_amdgcn_readfirstlane((u32)a) |
+                   ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(a >> 32)) << 32);
+    g.wlo = a0 - obase;
+    g.wlo &= ~(u64)15;
+    const u64 span = (hi - obase) - g.wlo;
+    g.wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    return g;
+  };
+  auto issue = [&](const WinGeo<WIN> &g, u32 *w) {
+    const uint8_t *src = bytes + g.wlo;
+#pragma unroll
+    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
+      if ((u32)j * 1024 < g.wbytes) {  // wave-uniform
+        if ((u32)j * 1024 + lane * 16 < g.wbytes)
+          __builtin_amdgcn_global_load_lds(
+              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+              (void __attribute__((address_space(3))) *)(w + 256 * j), 16, 0, AUX);
+      }
+    }
+  };
+  // a tile's digests are stored one step late, right after the next DMA is
+  // issued: the wait at the top of a step then only covers operations issued
+  // a whole tile of hashing earlier (on CDNA a load wait also waits for every
+  // older store)
+  typename Algo::Out h{};
+  u64 hi_pend = ~0ull;  // index of the digest held in h (~0: none)
+  auto hash = [&](u64 t, const WinGeo<WIN> &g, const u32 *w) {
+    const u64 i = (t << 6) + lane;
+    hi_pend = ~0ull;
+    if (i < n) {
+      const u64 len = g.end - g.start;
+      if (g.end - g.wlo <= g.wbytes)
+        h = algo(LdsReader{w, (u32)(g.start - g.wlo)}, len);
+      else
+        h = algo(GlobalReader{bytes + g.start}, len);
+      hi_pend = i;
+    }
+  };
+  auto put_pending = [&] {
+    if (hi_pend != ~0ull) sink.put(hi_pend, h);
+  };
+
+  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
+  if (t < ntiles) {
+    u64 a, hi, an, hin;
+    load_offs(t, a, hi);
+    WinGeo<WIN> g = geometry(a, hi), gn;
+    issue(g, wa);
+    // offsets loads are unconditional (clamped tile): a conditional load
+    // merges with the old value through a register copy, and the copy waits
+    // vmcnt(0) for the DMA issued just before it
+    const u64 last = ntiles - 1;
+    load_offs(min(t + nwaves, last), an, hin);
+    // one step: hash tile t out of `cur` while tile t+nwaves streams into `nxt`
+    auto step = [&](u32 *cur, u32 *nxt) -> bool {
+      const u64 tn = t + nwaves;
+      const bool more = tn < ntiles;  // wave-uniform
+      // tile t's DMA (issued one step ago) has landed; the compiler does not
+      // order LDS reads after LDS-DMA by itself, so this wait is what makes
+      // `cur` readable (it also covers the offsets loads of the same step)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (more) {
+        gn = geometry(an, hin);
+        issue(gn, nxt);
+      }
+      put_pending();
+      if (more) load_offs(min(tn + nwaves, last), an, hin);
+      hash(t, g, cur);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // `cur` is the DMA target two tiles on
+      g = gn;
+      t = tn;
+      return more;
+    };
+    while (step(wa, wb) && step(wb, wa)) {
+    }
+    put_pending();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   sink.flush();
 }
 

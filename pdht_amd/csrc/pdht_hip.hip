@@ -257,6 +257,21 @@ static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n
         k_window_pf<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
             b, offsets, obase, 0, 0, n, algo, sink);
         break;
+      case 23:
+        g_kernel = "k_window2<10224>";
+        k_window2<10224, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
+            b, offsets, obase, n, algo, sink_nt);
+        break;
+      case 24:
+        g_kernel = "k_window2<10224,def>";
+        k_window2<10224, Algo, SinkNt, 0><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
+            b, offsets, obase, n, algo, sink_nt);
+        break;
+      case 25:
+        g_kernel = "k_window2<6144>";
+        k_window2<6144, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
+            b, offsets, obase, n, algo, sink_nt);
+        break;
       case 11:
         g_kernel = "k_window<var,nt>";
         k_window<kWinBytes, true, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
@@ -758,6 +773,15 @@ PDHT_API int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out,
                                                                 AlgoFold64{}, sink);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+// Variable-length counterpart: the default offset-indexed kernel's data
+// movement (window DMA, offsets, LDS reads of every key byte, digest stores)
+// with an XOR fold for the hash.
+PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
+                                         uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_var(bytes, offsets, 0, n, AlgoFoldVar{}, Sink64{nullptr, out}, ST(s));
 }
 
 PDHT_API int pdht_hip_splitmix64_fill_dev(uint64_t seed, uint64_t first, size_t nwords,

@@ -179,6 +179,28 @@ def test_key_stream_calibration_kernel(dev, n):
     assert (got == want).all()
 
 
+def test_key_stream_var_calibration_kernel(dev):
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 300, 5000)
+    lens[7] = 20000  # past the LDS window
+    offs = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    data = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    got = u64(P.key_stream_var(to_dev(data, dev), to_dev(offs.astype(np.int64), dev)))
+    for i in range(lens.size):
+        k = data[int(offs[i]):int(offs[i + 1])]
+        m = len(k) // 16 * 16
+        w = k[:m].view(np.uint32).reshape(-1, 4)
+        a = int(len(k)) & 0xFFFFFFFF
+        b = 0
+        if m:
+            a ^= int(np.bitwise_xor.reduce(w[:, 0] ^ w[:, 2]))
+            b ^= int(np.bitwise_xor.reduce(w[:, 1] ^ w[:, 3]))
+        for o in range(m, len(k)):
+            a ^= int(k[o]) << (8 * (o & 3))
+        assert int(got[i]) == (b << 32) | a, i
+
+
 def test_errors_are_loud(dev):
     k = torch.zeros((4, 8), dtype=torch.uint8, device=dev)
     with pytest.raises(P.PdhtError):
@@ -198,7 +220,8 @@ def test_var_golden_mixed(dev, golden, oracle):
 
 VAR_KERNELS = {0: "auto", 3: "k_window<var>", 10: "k_var_sorted",
                11: "k_window<var,nt>", 12: "k_window<var,nt,10224>", 13: "k_window<var,nt,16K>",
-               14: "k_window_pf<var>"}
+               14: "k_window_pf<var>", 23: "k_window2<10224>", 24: "k_window2<10224,def>",
+               25: "k_window2<6144>"}
 
 
 def auto_var_kernel(total_bytes, n):
@@ -215,6 +238,29 @@ def test_var_edge_cases(dev, oracle, variant):
         assert P.last_kernel() == want
     finally:
         P.set_variant(old)
+
+
+@pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
+def test_var_many_tiles_per_wave(dev, oracle, variant):
+    """Enough keys that every wave of the persistent grid runs several tiles
+    (the double-buffered kernels' steady state), with a few keys longer than
+    any window and empty keys sprinkled in; ragged last tile."""
+    rng = np.random.default_rng(23)
+    n = 700_001
+    lens = rng.integers(0, 300, n)
+    lens[rng.integers(0, n, 40)] = 0
+    lens[rng.integers(0, n, 12)] = rng.integers(11000, 30000, 12)
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    data = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    old = P.set_variant(variant)
+    try:
+        got = u64(P.city64_var_batch(to_dev(data, dev), to_dev(offs.astype(np.int64), dev)))
+        kern = P.last_kernel()
+    finally:
+        P.set_variant(old)
+    assert variant == 0 or kern == VAR_KERNELS[variant]
+    assert (got == oracle.city64_var(data, offs)).all()
 
 
 def _var_edge_cases(dev, oracle):
@@ -411,7 +457,9 @@ def test_cfg4_crc128_16M_full_fold(dev, folds):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-def test_cfg3_64M_mixed_full_fold(dev, folds):
+@pytest.mark.parametrize("variant", [0, 23])
+def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
+    """8.7 GB of keys: offsets far past 2^31 and 2^32 (64-bit window math)."""
     f = folds["cfg3_city64_64M_mixed"]
     n = f["n"]
     lens = P.mixed_lengths(0x1E575EED1E575EED, 0, n, 16, 256, device=dev)
@@ -421,7 +469,11 @@ def test_cfg3_64M_mixed_full_fold(dev, folds):
     assert total == f["total_bytes"]
     words = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, (total + 7) // 8, device=dev)
     data = words.view(torch.uint8)[:total]
-    d = P.city64_var_batch(data, offs)
+    old = P.set_variant(variant)
+    try:
+        d = P.city64_var_batch(data, offs)
+    finally:
+        P.set_variant(old)
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 

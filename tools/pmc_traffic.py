@@ -33,11 +33,13 @@ def main():
     ap.add_argument("--algo-bytes-per-key", type=float, required=True)
     ap.add_argument("--dir", default="gpurun_out")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--fetch-dir", default=None, help="default: <dir>/pmc_FETCH_SIZE")
+    ap.add_argument("--write-dir", default=None, help="default: <dir>/pmc_WRITE_SIZE")
     a = ap.parse_args()
-    f_kib, nf = per_launch(os.path.join(a.dir, "pmc_FETCH_SIZE", "run_counter_collection.csv"),
-                           a.kernel, "FETCH_SIZE")
-    w_kib, nw = per_launch(os.path.join(a.dir, "pmc_WRITE_SIZE", "run_counter_collection.csv"),
-                           a.kernel, "WRITE_SIZE")
+    fd = a.fetch_dir or os.path.join(a.dir, "pmc_FETCH_SIZE")
+    wd = a.write_dir or os.path.join(a.dir, "pmc_WRITE_SIZE")
+    f_kib, nf = per_launch(os.path.join(fd, "run_counter_collection.csv"), a.kernel, "FETCH_SIZE")
+    w_kib, nw = per_launch(os.path.join(wd, "run_counter_collection.csv"), a.kernel, "WRITE_SIZE")
     fetch = f_kib * 1024 * 2  # gfx950: FETCH_SIZE = half of a wide streaming read
     write = w_kib * 1024
     algo = a.algo_bytes_per_key * a.keys
