@@ -385,21 +385,28 @@ constexpr Crc32cTables make_crc32c_tables() {
 __device__ __constant__ const Crc32cTables kCrcDev = make_crc32c_tables();
 static constexpr Crc32cTables kCrcHost = make_crc32c_tables();
 
-PDHT_HD u64 crc32c_u64(u64 crc, u64 v) {
+// Where the tables live: CrcConstTab = the compile-time tables (host; device
+// constant memory), kernels.h adds an LDS copy for the GPU's long-key path.
+struct CrcConstTab {
+  PDHT_HD u32 operator()(u32 slice, u32 byte) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const Crc32cTables &T = kCrcDev;
+    return kCrcDev.t[slice][byte];
 #else
-  const Crc32cTables &T = kCrcHost;
+    return kCrcHost.t[slice][byte];
 #endif
+  }
+};
+
+template <class Tab = CrcConstTab>
+PDHT_HD u64 crc32c_u64(u64 crc, u64 v, const Tab &T = Tab{}) {
   const u64 x = v ^ (u32)crc;
-  return T.t[7][x & 0xff] ^ T.t[6][(x >> 8) & 0xff] ^ T.t[5][(x >> 16) & 0xff] ^
-         T.t[4][(x >> 24) & 0xff] ^ T.t[3][(x >> 32) & 0xff] ^ T.t[2][(x >> 40) & 0xff] ^
-         T.t[1][(x >> 48) & 0xff] ^ T.t[0][x >> 56];
+  return T(7, x & 0xff) ^ T(6, (x >> 8) & 0xff) ^ T(5, (x >> 16) & 0xff) ^ T(4, (x >> 24) & 0xff) ^
+         T(3, (x >> 32) & 0xff) ^ T(2, (x >> 40) & 0xff) ^ T(1, (x >> 48) & 0xff) ^ T(0, (u32)(x >> 56));
 }
 
 // city.c:407-473 (CityHashCrc256Long), len >= 240
-template <class R>
-PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4]) {
+template <class R, class Tab = CrcConstTab>
+PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T = Tab{}) {
   u64 a = fetch64(s, 56) + kK0;
   u64 b = fetch64(s, 96) + kK0;
   u64 c = out[0] = mix16(b, len);
@@ -417,11 +424,11 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4]) {
     d = rotr(e, 33u ^ flip) * mult + q.w64(24);
     e = rotr(t, 25u ^ flip) * mult + q.w64(32);
     t = a0;
-    f = crc32c_u64(f, a);
-    g = crc32c_u64(g, b);
-    h = crc32c_u64(h, c);
-    i = crc32c_u64(i, d);
-    j = crc32c_u64(j, e);
+    f = crc32c_u64(f, a, T);
+    g = crc32c_u64(g, b, T);
+    h = crc32c_u64(h, c, T);
+    i = crc32c_u64(i, d, T);
+    j = crc32c_u64(j, e, T);
     o += 40;
   };
   const u64 blocks = len / 240;
@@ -460,32 +467,32 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4]) {
 }
 
 // city.c:476-489
-template <class R>
-PDHT_HD void crc256(const R &s, u64 len, u64 out[4]) {
+template <class R, class Tab = CrcConstTab>
+PDHT_HD void crc256(const R &s, u64 len, u64 out[4], const Tab &T = Tab{}) {
   if (len >= 240) {
-    crc256_long(s, len, 0u, out);
+    crc256_long(s, len, 0u, out, T);
   } else {
-    crc256_long(PadReader<R>{s, (u32)len}, 240, ~(u32)len, out);
+    crc256_long(PadReader<R>{s, (u32)len}, 240, ~(u32)len, out, T);
   }
 }
 
 // city.c:491-504
-template <class R>
-PDHT_HD u128 crc128_seed(const R &s, u64 len, u128 seed) {
+template <class R, class Tab = CrcConstTab>
+PDHT_HD u128 crc128_seed(const R &s, u64 len, u128 seed, const Tab &T = Tab{}) {
   if (len <= 900) return city128_seed(s, len, seed);
   u64 r[4];
-  crc256(s, len, r);
+  crc256(s, len, r, T);
   const u64 u = seed.hi + r[0];
   const u64 v = seed.lo + r[1];
   return u128{mix16(u, v + r[2]), mix16(rotr_nz(v, 32), u * kK0 + r[3])};
 }
 
 // city.c:506-517
-template <class R>
-PDHT_HD u128 crc128(const R &s, u64 len) {
+template <class R, class Tab = CrcConstTab>
+PDHT_HD u128 crc128(const R &s, u64 len, const Tab &T = Tab{}) {
   if (len <= 900) return city128(s, len);
   u64 r[4];
-  crc256(s, len, r);
+  crc256(s, len, r, T);
   return u128{r[2], r[3]};
 }
 

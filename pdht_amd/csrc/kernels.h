@@ -24,6 +24,7 @@
 
 namespace pdht {
 
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBlock = 256;  // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 
@@ -64,11 +65,30 @@ struct LdsReader {
 // it, i.e. wait for the next tile's prefetch on the common path too.
 typedef const __attribute__((address_space(1))) u32 gu32;
 typedef const __attribute__((address_space(1))) uint8_t gu8;
-struct GlobalReader {
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+template <bool A16 = false>
+struct GlobalReaderT {
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
+    if constexpr (A16 && N % 16 == 0) {
+      // packed keys at a 16-B multiple stride: 16-B aligned spans (every
+      // lane alike) load as dwordx4, a quarter of the instructions
+      if ((a & 15) == 0) {
+        gu32x4 *q = reinterpret_cast<gu32x4 *>(a);
+        Words<N / 4> w;
+#pragma unroll
+        for (int j = 0; j < N / 16; ++j) {
+          const u32x4 v = q[j];
+          w.d[4 * j + 0] = v.x;
+          w.d[4 * j + 1] = v.y;
+          w.d[4 * j + 2] = v.z;
+          w.d[4 * j + 3] = v.w;
+        }
+        return w;
+      }
+    }
     gu32 *q = reinterpret_cast<gu32 *>(a & ~(uintptr_t)3);
     const u32 r = (u32)(a & 3);
     u32 raw[N / 4 + 1];
@@ -85,6 +105,7 @@ struct GlobalReader {
     return reinterpret_cast<gu8 *>(reinterpret_cast<uintptr_t>(p))[o];
   }
 };
+typedef GlobalReaderT<false> GlobalReader;
 
 // ------------------------------------------------------------ algorithms ---
 struct AlgoCity64 {
@@ -126,6 +147,52 @@ struct AlgoCrc128Seed {
     return crc128_seed(r, len, u128{lo, hi});
   }
 };
+
+// CRC-32C slicing tables in LDS (8 KiB per workgroup) for batches that may
+// hold keys > 900 B (CityHashCrc256 path, city.c:407-517): one lookup per key
+// byte, 64 lanes at random table words.  From constant memory those lookups
+// are per-lane vector loads through the TA, 4x slower (tools/longbench.py).
+struct CrcLdsTab {
+  const u32 *t;
+  __device__ __forceinline__ u32 operator()(u32 slice, u32 byte) const { return t[slice * 256 + byte]; }
+};
+template <class Base>
+struct CrcLds : Base {
+  static constexpr bool kCrcLds = true;
+  const u32 *tab = nullptr;  // set by algo_init() inside the kernel
+  template <class R>
+  __device__ __forceinline__ typename Base::Out operator()(const R &r, u64 len) const;
+};
+template <>
+template <class R>
+__device__ __forceinline__ u128 CrcLds<AlgoCrc128>::operator()(const R &r, u64 len) const {
+  return crc128(r, len, CrcLdsTab{tab});
+}
+template <>
+template <class R>
+__device__ __forceinline__ u128 CrcLds<AlgoCrc128Seed>::operator()(const R &r, u64 len) const {
+  return crc128_seed(r, len, u128{this->lo, this->hi}, CrcLdsTab{tab});
+}
+
+template <class A, class = void>
+struct HasCrcLds {
+  static constexpr bool value = false;
+};
+template <class A>
+struct HasCrcLds<A, decltype((void)A::kCrcLds)> {
+  static constexpr bool value = A::kCrcLds;
+};
+
+// Per-workgroup algorithm setup, reached by every thread of the block.
+template <class Algo>
+__device__ __forceinline__ void algo_init(Algo &a) {
+  if constexpr (HasCrcLds<Algo>::value) {
+    __shared__ u32 tab[8 * 256];
+    for (u32 k = threadIdx.x; k < 8 * 256; k += blockDim.x) tab[k] = kCrcDev.t[k >> 8][k & 255];
+    __syncthreads();
+    a.tab = tab;
+  }
+}
 
 // Calibration only (pdht_hip_key_stream_dev): the data movement of a hash
 // kernel with the hash replaced by an XOR fold of the key's 64 bytes.
@@ -285,7 +352,6 @@ struct NtSink<SinkPlace> {
 };
 
 // ------------------------------------------------------------ key loads ---
-typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool NT, class T>
 __device__ __forceinline__ T ld(const T *p) {
@@ -510,6 +576,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
   __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
+  algo_init(algo);
   sink.init();
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lane = threadIdx.x & 63;
@@ -573,6 +640,35 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
   sink.flush();
 }
 
+// ---------------------------------------------------------- long keys ---
+// Keys far longer than a 64-key LDS window can hold (fixed L > 255 B): each
+// lane walks its own key straight from global memory (GlobalReader); the
+// other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
+// bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
+template <bool VAR, class Algo, class Sink, bool A16 = false>
+__global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ bytes,
+                                                   const u64 *__restrict__ offsets, u64 obase,
+                                                   u64 stride, u64 keylen, u64 n, Algo algo,
+                                                   Sink sink) {
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  algo_init(algo);
+  sink.init();
+  const u64 step = (u64)gridDim.x * kBlock;
+  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) {
+    u64 st, len;
+    if constexpr (VAR) {
+      st = offsets[i] - obase;
+      len = offsets[i + 1] - obase - st;
+    } else {
+      st = i * stride;
+      len = keylen;
+    }
+    sink.put(i, algo(GlobalReaderT<A16>{bytes + st}, len));
+  }
+  sink.flush();
+}
+
 // ------------------------------------------- double-buffered window kernel ---
 // Offset-indexed keys.  k_window with two LDS windows per wave: while tile t
 // hashes out of one window, the LDS-DMA of tile t+nwaves streams into the
@@ -599,6 +695,7 @@ __global__ __launch_bounds__(kBlock) void k_window2(const uint8_t *__restrict__ 
   __shared__ __attribute__((aligned(16))) u32 winB[kWavesPerBlock * (WIN / 4) + 4];
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
+  algo_init(algo);
   sink.init();
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lane = threadIdx.x & 63;
@@ -719,6 +816,7 @@ __global__ __launch_bounds__(kBlock) void k_window_pf(const uint8_t *__restrict_
   __shared__ __attribute__((aligned(16))) u32 win[kWavesPerBlock][WIN / 4 + 4];
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
+  algo_init(algo);
   sink.init();
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lane = threadIdx.x & 63;
@@ -823,6 +921,7 @@ __global__ __launch_bounds__(kBlock) void k_var_sorted(const uint8_t *__restrict
   __shared__ u32 s_rel[kBlock], s_len[kBlock], s_perm[kBlock], s_cnt[8];
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
+  algo_init(algo);
   sink.init();
   const u32 tid = threadIdx.x;
   const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -177,6 +177,11 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
         g_kernel = "k_fixed_xpose64<depth2>";
         k_fixed_xpose64<Algo, SinkNt, true, 2><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
         break;
+      case 26:
+        g_kernel = "k_fixed_xpose64<nt-load,plain-store>";
+        k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+            k, n, algo, sink);
+        break;
       case 1:
         g_kernel = "k_fixed_xpose64<plain>";
         k_fixed_xpose64<Algo, Sink, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink);
@@ -198,6 +203,8 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
     launch_small<8>(keylen, k, n, algo, sink, st, dev, blocks, variant);
   } else {
     const u64 tiles = (n + 63) / 64;
+    typedef typename NtSink<Sink>::type SinkNt;
+    const u64 tile_bytes = 63 * (u64)stride + keylen + 16;  // a 64-key tile + alignment slack
     if (variant == 3) {
       g_kernel = "k_window<fixed>";
       k_window<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
@@ -206,10 +213,29 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
       g_kernel = "k_window_pf<fixed>";
       k_window_pf<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
           k, nullptr, 0, stride, keylen, n, algo, sink);
-    } else {
-      typedef typename NtSink<Sink>::type SinkNt;
+    } else if (variant == 11) {
       g_kernel = "k_window<fixed,nt>";
       k_window<kWinBytes, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+    } else if (variant == 27 || (variant != 28 && tile_bytes > 16384)) {
+      // keys too long for a 64-key window (tools/longbench.py, r01)
+      // the 16-B reader measured equal to dword loads (longbench r01): variant only
+      if (al16 && stride % 16 == 0 && variant == 30) {
+        g_kernel = "k_global<fixed,a16>";
+        k_global<false, Algo, SinkNt, true><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+      } else {
+        g_kernel = "k_global<fixed>";
+        k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+      }
+    } else if (tile_bytes > 10224) {
+      g_kernel = "k_window<fixed,nt,16K>";
+      k_window<16384, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 2, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+    } else {
+      g_kernel = "k_window<fixed,nt,10224>";
+      k_window<10224, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 4, dev), kBlock, 0, st>>>(
           k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
     }
   }
@@ -257,6 +283,11 @@ static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n
         k_window_pf<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
             b, offsets, obase, 0, 0, n, algo, sink);
         break;
+      case 31:
+        g_kernel = "k_global<var>";
+        k_global<true, Algo, SinkNt><<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, sink_nt);
+        break;
       case 23:
         g_kernel = "k_window2<10224>";
         k_window2<10224, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
@@ -282,6 +313,8 @@ static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n
         // length (tools/varbench.py, r01): mean <= 160 B (cfg3's 16..256 mix,
         // mean 136) -> 10224 B at 4 workgroups/CU; longer -> 16 KiB at 2.
         // Without a byte-count hint (pdht_hip_set_var_bytes_hint) -> 10224.
+        // (k_global<var>, per-lane global reads, measured slower than the
+        // 16 KiB window even at 1-3 KiB keys: varbench r01)
         if (hint && hint / n > 160) {
           g_kernel = "k_window<var,nt,16K>";
           k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
@@ -549,18 +582,24 @@ PDHT_API int pdht_city128_batch_var_dev(const void *bytes, const uint64_t *offse
 PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
                                        uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
+  if (keylen > 900)  // CityHashCrc256 rounds: CRC-32C tables in LDS
+    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));
 }
 PDHT_API int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride, size_t keylen,
                                             size_t n, uint64_t lo, uint64_t hi, uint64_t *out,
                                             pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
+  if (keylen > 900)
+    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128Seed>{{lo, hi}}, Sink128{nullptr, out},
+                        ST(s));
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128Seed{lo, hi}, Sink128{nullptr, out}, ST(s));
 }
 PDHT_API int pdht_citycrc128_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
                                            uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
-  return launch_var(bytes, offsets, 0, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));
+  // any key may exceed 900 B (CityHashCrc256 rounds): CRC-32C tables in LDS
+  return launch_var(bytes, offsets, 0, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
 }
 
 PDHT_API int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
@@ -585,6 +624,9 @@ PDHT_API int pdht_citycrc128_batch_host(const void *keys, size_t keylen, size_t 
                                         int device) {
   return host_fixed(keys, keylen, n, 16, out, device,
                     [&](const uint8_t *dk, size_t cnt, uint8_t *dout, hipStream_t st) {
+                      if (keylen > 900)
+                        return launch_fixed(dk, keylen, keylen, cnt, CrcLds<AlgoCrc128>{},
+                                            Sink128{nullptr, reinterpret_cast<u64 *>(dout)}, st);
                       return launch_fixed(dk, keylen, keylen, cnt, AlgoCrc128{},
                                           Sink128{nullptr, reinterpret_cast<u64 *>(dout)}, st);
                     });

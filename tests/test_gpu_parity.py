@@ -55,6 +55,20 @@ def test_generator_matches_oracle(dev, oracle):
     assert (lens.cpu().numpy().astype(np.uint64) == oracle.mixed_lengths(5000)).all()
 
 
+def global_kernel(stride):
+    """k_global's default reader (dword loads; variant 30 = 16-B loads)."""
+    return "k_global<fixed>"
+
+
+def fixed_kernel(L, stride=None):
+    """launch_fixed's choice for a generic length: the LDS window that holds a
+    64-key tile (10224 B or 16 KiB), else per-lane global reads."""
+    tile = 63 * (stride or L) + L + 16
+    if tile > 16384:
+        return global_kernel(stride or L)
+    return "k_window<fixed,nt,16K>" if tile > 10224 else "k_window<fixed,nt,10224>"
+
+
 @pytest.mark.parametrize("L", list(range(0, 300)) + [511, 512, 899, 900, 901, 1000, 2047, 4097])
 def test_city64_every_length(dev, oracle, L):
     rng = np.random.default_rng(L)
@@ -65,9 +79,10 @@ def test_city64_every_length(dev, oracle, L):
     if L in (8, 16, 32, 64):
         assert P.last_kernel().startswith("k_fixed_"), P.last_kernel()
     else:
-        assert P.last_kernel() == "k_window<fixed,nt>"
-    if L in (13, 100, 1000):  # the other generic-length kernels too
-        for v, name in ((3, "k_window<fixed>"), (14, "k_window_pf<fixed>")):
+        assert P.last_kernel() == fixed_kernel(L)
+    if L in (13, 100, 200, 1000):  # the other generic-length kernels too
+        for v, name in ((3, "k_window<fixed>"), (14, "k_window_pf<fixed>"), (11, "k_window<fixed,nt>"),
+                        (27, global_kernel(L)), (28, fixed_kernel(min(L, 255)))):
             old = P.set_variant(v)
             try:
                 got = u64(P.city64_batch(to_dev(k, dev)))
@@ -77,7 +92,8 @@ def test_city64_every_length(dev, oracle, L):
             assert (got == oracle.city64_fixed(k)).all()
 
 
-@pytest.mark.parametrize("L", [0, 1, 3, 8, 13, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 144, 200, 901, 2000])
+@pytest.mark.parametrize("L", [0, 1, 3, 8, 13, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 144, 200, 256,
+                               899, 900, 901, 960, 2000, 4096])
 def test_city128_crc128_lengths(dev, oracle, L):
     rng = np.random.default_rng(1000 + L)
     n = 70
@@ -85,6 +101,45 @@ def test_city128_crc128_lengths(dev, oracle, L):
     kd = to_dev(k, dev)
     assert (u64(P.city128_batch(kd)) == oracle.city128_fixed(k)).all()
     assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
+
+
+@pytest.mark.parametrize("L", [256, 901, 1000, 4096])
+def test_long_keys_global_reader(dev, oracle, L):
+    """k_global with and without the 16-B reader (variant 30 asks for it; it
+    applies when every key starts 16-B aligned), aligned and misaligned base."""
+    rng = np.random.default_rng(L + 5)
+    n = 3000
+    flat = to_dev(rng.integers(0, 256, n * L + 16, dtype=np.uint8), dev)
+    for base in (0, 16, 4):
+        kd = flat[base:base + n * L].view(n, L)
+        want = oracle.city64_fixed(kd.cpu().numpy())
+        for v in (0, 30):
+            old = P.set_variant(v)
+            try:
+                got = u64(P.city64_batch(kd))
+                kern = P.last_kernel()
+            finally:
+                P.set_variant(old)
+            assert (got == want).all(), (base, v, kern)
+            if L > 255:
+                a16 = v == 30 and L % 16 == 0 and base % 16 == 0
+                assert kern == ("k_global<fixed,a16>" if a16 else "k_global<fixed>"), kern
+
+
+@pytest.mark.parametrize("L", [901, 1000, 4096])
+def test_crc128_long_keys_many_tiles(dev, oracle, L):
+    """CityHashCrc256 rounds with the LDS CRC tables, every workgroup of the
+    grid busy (k_global, 8 WG/CU) and a ragged tail; seeded variant too."""
+    rng = np.random.default_rng(L)
+    n = 256 * 8 * 256 + 77 if L == 901 else 70_001
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
+    assert P.last_kernel() == global_kernel(L)
+    s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
+    got = u64(P.citycrc128_seed_batch(kd[:300], (s0, s1))).reshape(-1, 2)
+    assert [tuple(int(x) for x in g) for g in got] == \
+        [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:300]]
 
 
 @pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 300, 1200])
@@ -108,7 +163,7 @@ VARIANT_KERNELS = {0: "k_fixed_xpose64", 1: "k_fixed_xpose64<plain>", 2: "k_fixe
                    4: "k_fixed_lds64<nt-store>", 5: "k_fixed_direct<64,1,nt-load,nt-store>",
                    6: "k_fixed_direct<64,1>", 7: "k_fixed_xpose64<depth1>",
                    8: "k_fixed_xpose64<nt-store>", 9: "k_fixed_direct<64,1,nt-store>",
-                   15: "k_fixed_xpose64<depth2>"}
+                   15: "k_fixed_xpose64<depth2>", 26: "k_fixed_xpose64<nt-load,plain-store>"}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANT_KERNELS))
@@ -147,7 +202,7 @@ def test_edge_layouts(dev, oracle):
     big = rng.integers(0, 256, (1000, 80), dtype=np.uint8)
     bd = to_dev(big, dev)
     got = u64(P.city64_batch(bd[:, :64]))
-    assert P.last_kernel() == "k_window<fixed,nt>"
+    assert P.last_kernel() == fixed_kernel(64, 80)
     assert (got == oracle.city64_fixed(big[:, :64])).all()
     flat = to_dev(rng.integers(0, 256, 64 * 777 + 1, dtype=np.uint8), dev)
     mis = flat[1:].view(777, 64)
@@ -221,7 +276,7 @@ def test_var_golden_mixed(dev, golden, oracle):
 VAR_KERNELS = {0: "auto", 3: "k_window<var>", 10: "k_var_sorted",
                11: "k_window<var,nt>", 12: "k_window<var,nt,10224>", 13: "k_window<var,nt,16K>",
                14: "k_window_pf<var>", 23: "k_window2<10224>", 24: "k_window2<10224,def>",
-               25: "k_window2<6144>"}
+               25: "k_window2<6144>", 31: "k_global<var>"}
 
 
 def auto_var_kernel(total_bytes, n):

@@ -19,7 +19,7 @@ import pdht_amd as P  # noqa: E402
 NAMES = {0: "xpose nt/nt depth 2, 3 WG/CU (default)", 1: "xpose plain", 2: "lds-dma+prefetch",
          3: "window", 4: "lds-dma nt-store", 5: "direct nt-load nt-store", 6: "direct plain",
          7: "xpose nt/nt depth 1, 4 WG/CU", 8: "xpose nt-store", 9: "direct nt-store",
-         15: "xpose nt/nt depth 2, 4 WG/CU"}
+         15: "xpose nt/nt depth 2, 4 WG/CU", 26: "xpose nt-load plain-store depth 2"}
 
 
 def main():

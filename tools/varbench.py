@@ -24,21 +24,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="0")
     ap.add_argument("--cases", default="mixed16-256,const136,const64,mixed129-256")
+    ap.add_argument("--max-bytes", type=int, default=3 << 30, help="cap on key bytes per case")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    n = a.n
-    data = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, n * 260 // 8, device=dev).view(torch.uint8)
-    gen = {
-        "mixed16-256": lambda: P.mixed_lengths(0x1E575EED1E575EED, 0, n, 16, 256, device=dev),
-        "const136": lambda: torch.full((n,), 136, dtype=torch.int64, device=dev),
-        "const200": lambda: torch.full((n,), 200, dtype=torch.int64, device=dev),
-        "const64": lambda: torch.full((n,), 64, dtype=torch.int64, device=dev),
-        "mixed65-128": lambda: P.mixed_lengths(0x1E575EED1E575EED, 0, n, 65, 128, device=dev),
-        "mixed129-256": lambda: P.mixed_lengths(0x1E575EED1E575EED, 0, n, 129, 256, device=dev),
+    data = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, a.max_bytes // 8, device=dev).view(torch.uint8)
+    S = 0x1E575EED1E575EED
+    cases = {  # name -> (lo, hi) uniform lengths
+        "mixed16-256": (16, 256), "const136": (136, 136), "const200": (200, 200), "const64": (64, 64),
+        "mixed65-128": (65, 128), "mixed129-256": (129, 256), "mixed256-768": (256, 768),
+        "mixed1k-3k": (1024, 3072),
     }
     variants = [int(x) for x in a.variants.split(",")]
     for case in a.cases.split(","):
-        lens = gen[case]()
+        lo, hi = cases[case]
+        n = min(a.n, a.max_bytes // hi)
+        lens = (torch.full((n,), lo, dtype=torch.int64, device=dev) if lo == hi
+                else P.mixed_lengths(S, 0, n, lo, hi, device=dev))
         offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         torch.cumsum(lens, 0, out=offs[1:])
         total = int(offs[-1].item())
