@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange"])
+                    choices=["cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange", "long"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (tools/kbench.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -145,6 +145,19 @@ def main():
             step = lambda: P.place_batch(keys, 3, 1024, hist=hist, out=outs)  # noqa: E731
             bytes_per_key = 8 + 8 + 4 + 4
             workload = f"place: fused pdht_hash (mbits+ptindex+rank+hist) over {n >> 20}M x 8B keys per GPU"
+        total_bytes_in = n * L
+    elif cfg == "long":
+        # f3: CityHashCrc128 above 900 B (CityHashCrc256 rounds, CRC-32C tables
+        # in LDS) over 1M x 1 KiB keys, device-resident
+        L = 1024
+        n = a.keys_per_gpu or M
+        sh = D.weak_shard(rank, world, n)
+        words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
+        keys = words.view(torch.uint8).view(n, L)
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        step = lambda: P.citycrc128_batch(keys, out=out)  # noqa: E731
+        bytes_per_key = L + 16
+        workload = f"long: CityHashCrc128 over {n >> 20}M x 1KiB keys per GPU (CRC-32C path), device-resident"
         total_bytes_in = n * L
     else:  # cfg3 mixed lengths
         L = None
@@ -320,11 +333,13 @@ def check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev):
         return f"unchecked (oracle unavailable: {e})"
     msgs = []
     s = min(sh.n, 65536)
-    if cfg in ("cfg2", "cfg4", "cfg5", "place"):
-        L = 8 if cfg == "place" else 64
+    if cfg in ("cfg2", "cfg4", "cfg5", "place", "long"):
+        L = {"place": 8, "long": 1024}.get(cfg, 64)
+        if cfg == "long":
+            s = min(s, 8192)
         k = O.fixed_keys(s, L, first_key=sh.first)
         got = out[:s].cpu().numpy().view(np.uint64)
-        if cfg == "cfg4":
+        if cfg in ("cfg4", "long"):
             ok = (got.reshape(-1, 2) == O.city128_fixed(k, crc=True)).all()
         elif cfg == "place":
             ok = (got == O.pdht_hash_fixed(k, 3, 1024)[0]).all()

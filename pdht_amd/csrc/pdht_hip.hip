@@ -214,8 +214,8 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
       k_window_pf<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
           k, nullptr, 0, stride, keylen, n, algo, sink);
     } else if (variant == 11) {
-      g_kernel = "k_window<fixed,nt>";
-      k_window<kWinBytes, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+      g_kernel = "k_window<fixed,nt,10224>";
+      k_window<10224, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 4, dev), kBlock, 0, st>>>(
           k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
     } else if (variant == 27 || (variant != 28 && tile_bytes > 16384)) {
       // keys too long for a 64-key window (tools/longbench.py, r01)
@@ -229,13 +229,13 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
         k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
       }
-    } else if (tile_bytes > 10224) {
+    } else if (tile_bytes > kWinBytes) {
       g_kernel = "k_window<fixed,nt,16K>";
       k_window<16384, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 2, dev), kBlock, 0, st>>>(
           k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
-    } else {
-      g_kernel = "k_window<fixed,nt,10224>";
-      k_window<10224, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 4, dev), kBlock, 0, st>>>(
+    } else {  // (10224 B at 4 WG/CU measured 2-4 % slower for fixed keys: longbench r01)
+      g_kernel = "k_window<fixed,nt>";
+      k_window<kWinBytes, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
           k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
     }
   }

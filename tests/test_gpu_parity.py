@@ -62,11 +62,11 @@ def global_kernel(stride):
 
 def fixed_kernel(L, stride=None):
     """launch_fixed's choice for a generic length: the LDS window that holds a
-    64-key tile (10224 B or 16 KiB), else per-lane global reads."""
+    64-key tile (12 KiB or 16 KiB), else per-lane global reads."""
     tile = 63 * (stride or L) + L + 16
     if tile > 16384:
         return global_kernel(stride or L)
-    return "k_window<fixed,nt,16K>" if tile > 10224 else "k_window<fixed,nt,10224>"
+    return "k_window<fixed,nt,16K>" if tile > 12288 else "k_window<fixed,nt>"
 
 
 @pytest.mark.parametrize("L", list(range(0, 300)) + [511, 512, 899, 900, 901, 1000, 2047, 4097])
@@ -81,7 +81,7 @@ def test_city64_every_length(dev, oracle, L):
     else:
         assert P.last_kernel() == fixed_kernel(L)
     if L in (13, 100, 200, 1000):  # the other generic-length kernels too
-        for v, name in ((3, "k_window<fixed>"), (14, "k_window_pf<fixed>"), (11, "k_window<fixed,nt>"),
+        for v, name in ((3, "k_window<fixed>"), (14, "k_window_pf<fixed>"), (11, "k_window<fixed,nt,10224>"),
                         (27, global_kernel(L)), (28, fixed_kernel(min(L, 255)))):
             old = P.set_variant(v)
             try:
