@@ -26,8 +26,9 @@ Rank 0 prints one JSON line.  Besides the contract fields it carries
                    sample of the same keys (rank 0, N = 1 only);
   host_resident -- the same hash with keys/digests in pinned host memory
                    (H2D + kernel + D2H pipeline), N = 1 only;
-  parity        -- this run's digests checked against the oracle (sample)
-                   and against the reference golden fold of every shard.
+  parity        -- this run's digests of the whole shard checked against the
+                   reference golden folds (tests/golden/config_folds.json);
+                   no oracle code runs outside the cpu_baseline leg.
 """
 from __future__ import annotations
 
@@ -245,7 +246,11 @@ def main():
     if bucketed is not None:
         parity = check_buckets(P, torch, D, sh, keys, bucketed, dev)
     else:
-        parity = check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev)
+        extra = None
+        if cfg == "place":  # one fresh call: the timed ones accumulated into hist
+            hist.zero_()
+            extra = (*P.place_batch(keys, 3, 1024, hist=hist), hist)
+        parity = check_parity(P, torch, D, cfg, sh, out, extra, dev)
 
     # ------------------------------------------------------- report ------
     value = n * world * a.steps / elapsed / 1e9
@@ -279,7 +284,7 @@ def main():
     if rank == 0 and world == 1 and cfg in ("cfg2", "cfg4") and not a.no_host:
         res["host_resident"] = host_rate(P, torch, n, cfg)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and cfg == "cfg2":
-        res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(a.cpu_seconds, out)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -317,6 +322,10 @@ def golden_shard_fold(folds, cfg, sh):
                 return int(c5["shards"][j], 16), f"cfg5 shard {j}"
         if sh.first == 0 and sh.n == 16 * M:
             return int(folds["cfg2_city64_16M_x64"]["total"], 16), "cfg2 total"
+    if cfg == "long" and sh.n == M and sh.first % M == 0:
+        g = folds.get("long_crc128_1M_x1024", {}).get("shards", [])
+        if sh.first // M < len(g):
+            return int(g[sh.first // M], 16), f"long shard {sh.first // M}"
     if cfg == "cfg4" and sh.first == 0 and sh.n == 16 * M:
         return int(folds["cfg4_crc128_16M_x64"]["total"], 16), "cfg4 total"
     if cfg == "cfg3" and sh.rank == 0 and sh.n == 64 * M:
@@ -324,65 +333,64 @@ def golden_shard_fold(folds, cfg, sh):
     return None, None
 
 
-def check_parity(P, torch, D, cfg, sh, out, keys, data, offs, dev):
-    """Bit-exact check of this rank's digests: a sample against the oracle
-    and the whole shard's fold against the reference golden fold."""
-    try:
-        from oracle import oracle as O
-    except Exception as e:  # pragma: no cover
-        return f"unchecked (oracle unavailable: {e})"
-    msgs = []
-    s = min(sh.n, 65536)
-    if cfg in ("cfg2", "cfg4", "cfg5", "place", "long"):
-        L = {"place": 8, "long": 1024}.get(cfg, 64)
-        if cfg == "long":
-            s = min(s, 8192)
-        k = O.fixed_keys(s, L, first_key=sh.first)
-        got = out[:s].cpu().numpy().view(np.uint64)
-        if cfg in ("cfg4", "long"):
-            ok = (got.reshape(-1, 2) == O.city128_fixed(k, crc=True)).all()
-        elif cfg == "place":
-            ok = (got == O.pdht_hash_fixed(k, 3, 1024)[0]).all()
+def check_parity(P, torch, D, cfg, sh, out, extra, dev):
+    """Bit-exact check of this rank's WHOLE shard against the reference golden
+    folds (tests/golden/config_folds.json: data generated from the reference
+    city.c by tests/golden/gen_golden.py).  No oracle code runs here; the
+    cpu_baseline leg separately compares the reference's own digests of its
+    sample with this run's GPU digests."""
+    folds = golden_folds()
+    if folds is None:
+        return "unchecked (tests/golden/config_folds.json missing)"
+    msgs, ok = [], True
+    if cfg == "place":
+        r = sh.first // (16 * M)
+        g = folds.get("place_8B_16M", {}).get("shards", [])
+        if sh.n == 16 * M and sh.first % (16 * M) == 0 and r < len(g):
+            mb, pt, rk, hist = extra
+            got = {"mbits": D.fold_tensor(mb, sh.first),
+                   "ptindex": D.fold_tensor(pt.to(torch.int64) & 0xFFFFFFFF, sh.first),
+                   "rank": D.fold_tensor(rk.to(torch.int64) & 0xFFFFFFFF, sh.first),
+                   "hist": D.fold_tensor(hist, 0)}
+            bad = [k for k, v in got.items() if v != int(g[r][k], 16)]
+            ok = not bad
+            msgs.append(f"mbits, ptindex, rank and histogram folds {'==' if ok else '!='} reference "
+                        f"golden (place shard {r})" + (f" (mismatch: {bad})" if bad else ""))
         else:
-            ok = (got == O.city64_fixed(k)).all()
+            msgs.append("no golden fold for this shard")
     else:
-        o = offs[: s + 1].cpu().numpy().astype(np.uint64)
-        d = data[: int(o[-1])].cpu().numpy()
-        ok = (out[:s].cpu().numpy().view(np.uint64) == O.city64_var(d, o)).all()
-    msgs.append(f"{s} keys vs oracle {'ok' if ok else 'MISMATCH'}")
-    want, what = golden_shard_fold(golden_folds(), cfg, sh)
-    fold_ok = True
-    if want is not None:
-        first_idx = 2 * sh.first if cfg == "cfg4" else sh.first
-        fold_ok = D.fold_tensor(out, first_idx) == want
-        msgs.append(f"full-shard fold {'==' if fold_ok else '!='} reference golden ({what})")
-    all_ok = D.allreduce_min_flag(bool(ok) and fold_ok, device=dev)
+        want, what = golden_shard_fold(folds, cfg, sh)
+        if want is not None:
+            first_idx = 2 * sh.first if cfg in ("cfg4", "long") else sh.first
+            ok = D.fold_tensor(out, first_idx) == want
+            msgs.append(f"full-shard fold {'==' if ok else '!='} reference golden ({what})")
+        else:
+            msgs.append("no golden fold for this shard")
+    all_ok = D.allreduce_min_flag(bool(ok), device=dev)
     if sh.world > 1:
         msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
     return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
 
 
 def check_buckets(P, torch, D, sh, keys, b, dev):
-    """Bucketing checks: a sample of buckets against the oracle's placement
-    (stable order), and full-size properties on the device -- index is a
+    """Bucketing checks without oracle code: the whole shard's bucketed mbits,
+    original indices and bucket offsets against the reference golden folds
+    (bucket config), and full-size properties on the device -- index is a
     permutation, ranks are non-decreasing, indices increase inside a bucket,
     keys_out == keys[index], mbits == CityHash64(keys_out)."""
-    try:
-        from oracle import oracle as O
-    except Exception as e:  # pragma: no cover
-        return f"unchecked (oracle unavailable: {e})"
     nr, ko, mb, ix, offs = b["nranks"], b["ko"], b["mb"], b["ix"], b["offs"]
     n = ix.numel()
-    msgs = []
-    s = min(n, 65536)
-    ks = O.fixed_keys(s, 8, first_key=sh.first)
-    m2, _, r2 = O.pdht_hash_fixed(ks, 3, nr)
-    order = np.argsort(r2, kind="stable")
-    # positions of the sample keys (index < s) inside the full bucketed output
-    ixc = ix.cpu().numpy()
-    sel = ixc < s
-    ok = bool((ixc[sel] == order).all() and (mb.cpu().numpy().view(np.uint64)[sel] == m2[order]).all())
-    msgs.append(f"first {s} keys bucketed as the oracle {'ok' if ok else 'MISMATCH'}")
+    msgs, ok = [], True
+    folds = golden_folds() or {}
+    g = folds.get("bucket_8B_16M", {})
+    r = sh.first // (16 * M)
+    if nr == g.get("nranks") and n == g.get("n") and sh.first % n == 0 and r < len(g.get("shards", [])):
+        gs = g["shards"][r]
+        got = {"mbits": D.fold_tensor(mb, 0), "index": D.fold_tensor(ix, 0), "offsets": D.fold_tensor(offs, 0)}
+        bad = [k for k, v in got.items() if v != int(gs[k], 16)]
+        ok = not bad
+        msgs.append(f"bucketed mbits, index and offsets folds {'==' if ok else '!='} reference golden "
+                    f"(bucket shard {r})" + (f" (mismatch: {bad})" if bad else ""))
     srt = torch.sort(ix).values
     perm = bool((srt == torch.arange(n, device=dev)).all().item())
     same = bool((ko == keys[ix]).all().item()) and bool((P.city64_batch(ko) == mb).all().item())
@@ -398,9 +406,11 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
         got_m = xm.cpu().numpy().view(np.uint64)
         mine = bool((got_m % np.uint64(sh.world) == np.uint64(sh.rank)).all())
         mine = mine and bool((P.city64_batch(xk) == xm).all().item())
-        xk_np, xi_np = xk.cpu().numpy(), xi.cpu().numpy()
-        for j in range(0, xi.numel(), max(1, xi.numel() // 256)):  # received key j is global key xi[j]
-            mine = mine and bool((xk_np[j] == O.fixed_keys(1, 8, first_key=int(xi_np[j]))[0]).all())
+        # received key j is global key xi[j]: regenerate it with the device
+        # generator (pinned to the oracle by tests/test_gpu_parity.py)
+        for j in range(0, xi.numel(), max(1, xi.numel() // 256)):
+            want = P.splitmix64_fill(SEED_KEYS, int(xi[j].item()), 1, device=dev)
+            mine = mine and bool((xk[j].view(torch.int64) == want).all().item())
         msgs.append(f"exchange: {xi.numel()} keys received, all owned by this rank {'ok' if mine else 'FAILED'}")
         ok = ok and mine
     all_ok = D.allreduce_min_flag(ok, device=dev)
@@ -432,9 +442,11 @@ def host_rate(P, torch, n, cfg):
         return {"error": str(e)}
 
 
-def cpu_baseline(budget_s: float):
+def cpu_baseline(budget_s: float, gpu_digests=None):
     """Reference city.c (oracle/_ref) on this host's cores over a bounded
-    sample: 4M x 64B keys of the same stream, repeated to fill ~budget_s."""
+    sample: 4M x 64B keys of the same stream, repeated to fill ~budget_s.
+    The reference's digests of the sample are compared with this run's GPU
+    digests of the same keys (gpu_digests: the first 4M of rank 0's batch)."""
     from oracle import oracle as O
     threads = min(16, os.cpu_count() or 1)
     s = 4 * M
@@ -442,12 +454,15 @@ def cpu_baseline(budget_s: float):
     secs, out, kind = O.time_city64(keys, threads, 1)
     reps = max(1, int(budget_s / max(secs, 1e-6)))
     secs, out, kind = O.time_city64(keys, threads, reps)
-    ok = bool((out[:4096] == O.city64_fixed(keys[:4096])).all())
+    ok = None
+    if gpu_digests is not None:
+        ok = bool((out == gpu_digests[:s].cpu().numpy().view(np.uint64)).all())
     one, _, _ = O.time_city64(keys[: M // 2], 1, 1)
     return {"value": round(s * reps / secs / 1e9, 4), "unit": "Gkeys/s", "cores": threads,
             "kind": kind, "sample": f"{reps} passes over 4M x 64B keys ({threads} pthreads, "
                                     f"{secs:.2f} s wall, {secs * threads:.1f} CPU-s)",
-            "single_thread_Gkeys_s": round((M // 2) / one / 1e9, 4), "digests_ok": ok}
+            "single_thread_Gkeys_s": round((M // 2) / one / 1e9, 4),
+            "gpu_digests_equal_reference": ok}
 
 
 if __name__ == "__main__":

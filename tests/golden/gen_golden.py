@@ -13,6 +13,7 @@ the two modulo reductions of hash.c:27 and :29 done in Python.
 
   python tests/golden/gen_golden.py          # small fixtures (seconds)
   python tests/golden/gen_golden.py --full   # + full-config fold checksums
+  python tests/golden/gen_golden.py --extra  # + place/bucket/long folds (added)
 """
 from __future__ import annotations
 
@@ -175,14 +176,66 @@ def folds_full(R) -> dict:
     return res
 
 
+def folds_extra() -> dict:
+    """Folds for the bench's secondary configs, per 16M-key weak-scaling shard
+    r = 0..7 (keys [r*16M, (r+1)*16M) of the stream), from the reference
+    CityHash64 / CityHashCrc128 plus hash.c:27/:29's two reductions:
+      place  (8-B keys, nptes 3, nranks 1024): folds of mbits, ptindex, rank
+             and the rank histogram;
+      bucket (8-B keys, nptes 3, nranks 1024): the stable bucketing of the
+             shard: folds of the bucketed mbits, of the original indices and
+             of the bucket offsets;
+      long   (1M x 1 KiB keys, CityHashCrc128 > 900 B = CityHashCrc256 path):
+             fold per shard of 1M keys."""
+    thr = os.cpu_count() or 8
+    res = {"place_8B_16M": {"n": 16 * M, "L": 8, "nptes": 3, "nranks": 1024, "shards": []},
+           "bucket_8B_16M": {"n": 16 * M, "L": 8, "nptes": 3, "nranks": 1024, "shards": []},
+           "long_crc128_1M_x1024": {"n": M, "L": 1024, "shards": []}}
+    n = 16 * M
+    for r in range(8):
+        keys = O.fixed_keys(n, 8, first_key=r * n)
+        m = O.apply_ref64(keys, n, L=8, threads=thr)
+        pt = (m % np.uint64(3)).astype(np.uint64)
+        rk = (m % np.uint64(1024)).astype(np.uint64)
+        hist = np.bincount(rk.astype(np.int64), minlength=1024).astype(np.uint64)
+        res["place_8B_16M"]["shards"].append({
+            "mbits": f"{O.fold64(m, r * n):016x}", "ptindex": f"{O.fold64(pt, r * n):016x}",
+            "rank": f"{O.fold64(rk, r * n):016x}", "hist": f"{O.fold64(hist, 0):016x}"})
+        order = np.argsort(rk, kind="stable")
+        offs = np.zeros(1025, np.uint64)
+        np.cumsum(hist, out=offs[1:])
+        res["bucket_8B_16M"]["shards"].append({
+            "mbits": f"{O.fold64(m[order], 0):016x}", "index": f"{O.fold64(order.astype(np.uint64), 0):016x}",
+            "offsets": f"{O.fold64(offs, 0):016x}"})
+        print(f"  place/bucket shard {r} done", flush=True)
+    nl = M
+    for r in range(8):
+        keys = O.fixed_keys(nl, 1024, first_key=r * nl)
+        d = O.apply_ref128(keys, nl, L=1024, threads=thr, fn_name="CityHashCrc128")
+        res["long_crc128_1M_x1024"]["shards"].append(f"{O.fold64(d.reshape(-1), 2 * r * nl):016x}")
+        print(f"  long shard {r} done", flush=True)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true")
+    ap.add_argument("--extra", action="store_true",
+                    help="add the place/bucket/long folds to config_folds.json")
     a = ap.parse_args()
     O.build()
     R = O.ref()
     if R is None:
         sys.exit("oracle/_ref not built: /root/reference is required to regenerate fixtures")
+    if a.extra:
+        path = os.path.join(HERE, "config_folds.json")
+        with open(path) as f:
+            doc = json.load(f)
+        doc["configs"].update(folds_extra())
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print("added place/bucket/long folds to config_folds.json")
+        return
     vec = small(R)
     np.savez_compressed(os.path.join(HERE, "city_golden.npz"), **vec)
     print("wrote city_golden.npz", os.path.getsize(os.path.join(HERE, "city_golden.npz")), "bytes")
