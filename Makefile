@@ -17,7 +17,8 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
 CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
 HIP_SRC := pdht_amd/csrc/pdht_hip.hip pdht_amd/csrc/city_host.hip
-HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h include/pdht_hip.h include/pdht_city.h
+HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/bucket.h \
+           include/pdht_hip.h include/pdht_city.h
 OBJ     := $(LIBDIR)/pdht_hip.o $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash.o
 
 .PHONY: all product oracle clean asm

@@ -170,6 +170,12 @@ int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out, pdht_hip_
  * replaced by an XOR fold (out[i] = fold of key i; see tests). */
 int pdht_hip_key_stream_var_dev(const void *bytes, const uint64_t *offsets, size_t n, uint64_t *out,
                                 pdht_hip_stream_t stream);
+/* Tuning only (tools/bucketbench.py): while buf != NULL (device memory, at
+ * least 16 uint64, zeroed by the caller), the bucketing scatter kernels add
+ * the shader-clock cycles their workgroups spend in each phase into buf[0..5]
+ * and the number of tiles into buf[8].  NULL (the default) turns it off.
+ * Returns 0. */
+int pdht_hip_set_phase_counters(uint64_t *buf);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,7 @@ def _declare(L):
         "pdht_hip_last_kernel": (C.c_char_p, []),
         "pdht_hip_set_var_bytes_hint": (C.c_int, [C.c_uint64]),
         "pdht_hip_set_variant": (C.c_int, [C.c_int]),
+        "pdht_hip_set_phase_counters": (C.c_int, [_V]),
         "pdht_hip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
         "pdht_hip_set_device": (C.c_int, [C.c_int]),
         "pdht_city64_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
@@ -151,6 +152,13 @@ def last_kernel() -> str:
 
 def set_variant(v: int) -> int:
     return lib().pdht_hip_set_variant(v)
+
+
+def set_phase_counters(buf=None) -> None:
+    """Tuning only: per-phase clock totals of the bucketing scatter kernels are
+    added into buf (int64[>=16], CUDA, zeroed) while set; None turns it off."""
+    _check(lib().pdht_hip_set_phase_counters(_dptr(buf) if buf is not None else None),
+           "pdht_hip_set_phase_counters")
 
 
 def device_count() -> int:
@@ -368,14 +376,20 @@ def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=
     return mb, pt, rk
 
 
+def bucket_workspace_bytes(n: int, nranks: int) -> int:
+    return lib().pdht_bucket_workspace_bytes(n, nranks)
+
+
 def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=True,
-                 with_index=True, stream=None):
+                 with_index=True, stream=None, out=None, workspace=None):
     """Destination bucketing (include/pdht_hip.h pdht_bucket_batch_dev): a stable
     counting sort of packed keys [n, L] by rank = CityHash64 % nranks.
 
     Returns (keys_out [n, L] | None, mbits int64[n], ptindex int32[n] | None,
     index int64[n] | None, offsets int64[nranks+1]); bucket r is rows
-    offsets[r]:offsets[r+1], keys in original order.
+    offsets[r]:offsets[r+1], keys in original order.  `out` = a previous
+    return value to reuse its tensors; `workspace` = a uint8 CUDA tensor of at
+    least bucket_workspace_bytes(n, nranks) bytes (allocated per call if None).
     """
     torch = _torch()
     n, L, stride = _keys_2d(keys)
@@ -383,12 +397,21 @@ def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=
         raise ValueError("bucket_batch needs packed keys")
     dev = keys.device
     ws_bytes = lib().pdht_bucket_workspace_bytes(n, nranks)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    ko = torch.empty_like(keys) if with_keys else None
-    mb = torch.empty(n, dtype=torch.int64, device=dev)
-    pt = torch.empty(n, dtype=torch.int32, device=dev) if with_ptindex else None
-    ix = torch.empty(n, dtype=torch.int64, device=dev) if with_index else None
-    offs = torch.empty(nranks + 1, dtype=torch.int64, device=dev)
+    if workspace is None:
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    else:
+        ws = workspace
+        if ws.numel() * ws.element_size() < ws_bytes:
+            raise ValueError(f"workspace smaller than {ws_bytes} bytes")
+        ws_bytes = ws.numel() * ws.element_size()
+    if out is not None:
+        ko, mb, pt, ix, offs = out
+    else:
+        ko = torch.empty_like(keys) if with_keys else None
+        mb = torch.empty(n, dtype=torch.int64, device=dev)
+        pt = torch.empty(n, dtype=torch.int32, device=dev) if with_ptindex else None
+        ix = torch.empty(n, dtype=torch.int64, device=dev) if with_index else None
+        offs = torch.empty(nranks + 1, dtype=torch.int64, device=dev)
     p = lambda t: _dptr(t) if t is not None else None  # noqa: E731
     _check(lib().pdht_bucket_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(ws), ws_bytes, p(ko),
                                        _dptr(mb), p(pt), p(ix), _dptr(offs), _stream_ptr(stream)),

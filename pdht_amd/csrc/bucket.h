@@ -225,6 +225,51 @@ __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW wo
   return off + x - v;
 }
 
+// Stable tile-local slots of a wave's KPL groups of 64 keys.  Lanes with the
+// same bucket find each other by ballots; each group's leader (its lowest
+// lane) claims the bucket's next run of slots with one returning LDS atomic on
+// the wave's own slot table.  A wave's LDS operations execute in issue order,
+// so the KPL atomics go out back to back (group g sees the increments of the
+// groups before it) and a single wait precedes the shuffles that hand every
+// lane its leader's base: two LDS round trips per tile instead of two per
+// group (rank_groups_serial).
+template <int KPL>
+__device__ __forceinline__ void rank_groups(u32 *myrun, const u32 (&rr)[KPL], u32 q0, u32 tn,
+                                            u32 nbits, u32 (&lp)[KPL]) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1;
+  u32 al[KPL], base[KPL];  // al = ahead | leader lane << 8
+#pragma unroll
+  for (int g = 0; g < KPL; ++g) {
+    const bool valid = q0 + g * 64 < tn;
+    const u64 same = same_bucket_lanes(valid, rr[g], nbits);
+    const u32 ahead = (u32)__builtin_popcountll(same & below);
+    al[g] = ahead | ((same ? (u32)__builtin_ctzll(same) : 0u) << 8);
+    base[g] = 0;
+    if (valid && ahead == 0) base[g] = atomicAdd(&myrun[rr[g]], (u32)__builtin_popcountll(same));
+  }
+#pragma unroll
+  for (int g = 0; g < KPL; ++g) lp[g] = (u32)__shfl((int)base[g], (int)(al[g] >> 8)) + (al[g] & 0xffu);
+}
+
+// The same, one group at a time (two LDS round trips per group).
+template <int KPL>
+__device__ __forceinline__ void rank_groups_serial(u32 *myrun, const u32 (&rr)[KPL], u32 q0, u32 tn,
+                                                   u32 nbits, u32 (&lp)[KPL]) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1;
+#pragma unroll
+  for (int g = 0; g < KPL; ++g) {
+    const bool valid = q0 + g * 64 < tn;
+    const u64 same = same_bucket_lanes(valid, rr[g], nbits);
+    const u32 ahead = (u32)__builtin_popcountll(same & below);
+    lp[g] = valid ? myrun[rr[g]] + ahead : 0;
+    wave_lds_sync();
+    if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
+    wave_lds_sync();
+  }
+}
+
 template <int L>
 __device__ __forceinline__ void store_key_row(uint8_t *dst, const RegReader<L / 4> &k) {
   if constexpr (L == 8) {
@@ -236,6 +281,39 @@ __device__ __forceinline__ void store_key_row(uint8_t *dst, const RegReader<L / 
       reinterpret_cast<u32x4 *>(dst)[j] = u32x4{k.d[4 * j], k.d[4 * j + 1], k.d[4 * j + 2], k.d[4 * j + 3]};
   }
 }
+
+// Tuning only (pdht_hip_set_phase_counters): shader-clock cycles per phase of
+// a scatter kernel, summed over workgroups.  Marks sit right after barriers,
+// so thread 0's clock stands for the workgroup's.  out == nullptr: off (one
+// scalar branch per mark).
+// ON = false (production instantiations): every member is a no-op.
+template <bool ON>
+struct PhaseClock {
+  u64 *out;
+  u64 last = 0;
+  u64 acc[6] = {0, 0, 0, 0, 0, 0};
+  u64 tiles = 0;
+  __device__ __forceinline__ explicit PhaseClock(u64 *o) : out(o) {
+    if (ON && out) last = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void tile() {
+    if (ON) ++tiles;
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (ON && out) {
+      const u64 now = __builtin_amdgcn_s_memtime();
+      acc[k] += now - last;
+      last = now;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    if (ON && out && threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) atomicAdd(reinterpret_cast<unsigned long long *>(out + k), acc[k]);
+      atomicAdd(reinterpret_cast<unsigned long long *>(out + 8), tiles);
+    }
+  }
+};
 
 // ------------------------------------------------------ staged scatter ---
 // Tile = 4 waves x 16 groups x 64 lanes = 4096 keys; wave w owns the
@@ -256,11 +334,14 @@ constexpr u32 kStTile = kStW * kStKPL * 64;
 constexpr size_t staged_lds_bytes(u32 nranks) {
   return (size_t)kStTile * 8 + (size_t)kStTile * 2 + (size_t)kStW * nranks * 4 + (size_t)nranks * 4;
 }
-template <int L>
-__global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
+// DBG (timing-only builds, tools/bucketbench.py; results are wrong): bit 0 =
+// identity ranking, 1 = no staging writes, 2 = no mbits/ptindex/index stores,
+// 3 = no key stores.
+template <int L, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false>
+__global__ __launch_bounds__(kStW * 64, L == 8 ? 2 : 1) void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
     TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
-    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out) {
+    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out, u64 *__restrict__ prof) {
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                              // [kStTile]
   uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kStTile);  // [kStTile]
@@ -269,14 +350,15 @@ __global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
   __shared__ u32 scan_scratch[kStW];
   constexpr u32 kSub = kStKPL * 64;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const u64 below = (1ull << lane) - 1;
   u32 *myrun = run + wave * nranks;
   const u32 per = (nranks + kBlock - 1) / kBlock;
   const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
+  PhaseClock<PROF> pc(prof);
   for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kStTile;
     const u32 tn = (u32)min((u64)kStTile, n - tbase);
+    pc.tile();
     for (u32 j = threadIdx.x; j < kStW * nranks; j += kBlock) run[j] = 0;
     const u32 q0 = wave * kSub + lane;
     RegReader<L / 4> kr[kStKPL];
@@ -290,10 +372,12 @@ __global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
       rr[g] = (u32)rk.mod(h[g]);
     }
     __syncthreads();
+    pc.mark(0);
 #pragma unroll
     for (int g = 0; g < kStKPL; ++g)
       if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
     __syncthreads();
+    pc.mark(1);
     u32 s = 0;
     for (u32 r = rb0; r < rb1; ++r)
 #pragma unroll
@@ -309,22 +393,24 @@ __global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
       }
     }
     __syncthreads();
+    pc.mark(2);
     u32 lp[kStKPL];
+    if constexpr (DBG & 1) {
 #pragma unroll
-    for (int g = 0; g < kStKPL; ++g) {
-      const bool valid = q0 + g * 64 < tn;
-      const u64 same = same_bucket_lanes(valid, rr[g], nbits);
-      const u32 ahead = (u32)__builtin_popcountll(same & below);
-      lp[g] = valid ? myrun[rr[g]] + ahead : 0;
-      wave_lds_sync();
-      if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
-      if (valid) {
+      for (int g = 0; g < kStKPL; ++g) lp[g] = q0 + g * 64;
+    } else if constexpr (BATCHED_RANK) {
+      rank_groups<kStKPL>(myrun, rr, q0, tn, nbits, lp);
+    } else {
+      rank_groups_serial<kStKPL>(myrun, rr, q0, tn, nbits, lp);
+    }
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g)
+      if (!(DBG & 2) && q0 + g * 64 < tn) {
         stage[lp[g]] = h[g];
         sidx[lp[g]] = (uint16_t)(q0 + g * 64);
       }
-      wave_lds_sync();
-    }
     __syncthreads();
+    pc.mark(3);
     constexpr int kPer = kStTile / kBlock;
     u32 gp[kPer];
 #pragma unroll
@@ -333,12 +419,13 @@ __global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
       if (j < tn) {
         const u64 hv = stage[j];
         gp[jj] = delta[(u32)rk.mod(hv)] + j;
+        if (DBG & 4) continue;
         mbits_out[gp[jj]] = hv;
         if (ptindex_out) ptindex_out[gp[jj]] = (u32)pt.mod(hv);
         if (index_out) index_out[gp[jj]] = tbase + sidx[j];
       }
     }
-    if (keys_out) {
+    if (keys_out && !(DBG & 8)) {
 #pragma unroll
       for (int c = 0; c < L / 8; ++c) {
         __syncthreads();
@@ -355,7 +442,152 @@ __global__ __launch_bounds__(kStW * 64) void k_bucket_scatter_staged(
       }
     }
     __syncthreads();
+    pc.mark(5);
   }
+  pc.flush();
+}
+
+// ------------------------------------------------ pipelined staged scatter ---
+// 8-B keys.  The staged scatter's phases, reordered so that no load waits for
+// this tile's stores: on gfx9 vmcnt retires in issue order, so a load wait
+// also waits for every store issued before the load.  Per tile:
+//   A/B/C as in _staged, with the tile starts (counts + chunk prefix rows,
+//         loaded with the keys) and the bucket bases (constant, loaded once)
+//         already in registers;
+//   D: each thread gathers its 16 staged digests, indices and -- through the
+//      same buffer -- keys into registers, computing the global slots;
+//   P: the NEXT tile's keys and tile starts are issued;
+//   S: all stores of this tile (mbits, ptindex, index, keys) from registers.
+// The loads of P retire before the stores of S, so the next tile's first
+// wait covers only them.  Needs every output (keys, ptindex, index).
+constexpr u32 kPipeRPT = kStagedMaxRanks / kBlock;  // ranks per thread (8)
+constexpr size_t pipe_lds_bytes(u32 nranks) { return staged_lds_bytes(nranks) + (size_t)nranks * 4; }
+template <bool PROF = false>
+__global__ __launch_bounds__(kStW * 64, 2) void k_bucket_scatter_pipe8(
+    const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
+    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
+    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out, u64 *__restrict__ prof) {
+  extern __shared__ u64 lds64[];
+  u64 *stage = lds64;                                              // [kStTile]
+  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kStTile);  // [kStTile]
+  u32 *run = reinterpret_cast<u32 *>(sidx + kStTile);              // [kStW][nranks]
+  u32 *delta = run + kStW * nranks;                                // [nranks]
+  u32 *bse = delta + nranks;  // [nranks] low words of the bucket bases (slots < 2^32)
+  __shared__ u32 scan_scratch[kStW];
+  constexpr u32 kSub = kStKPL * 64;
+  constexpr int kPer = kStTile / kBlock;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  u32 *myrun = run + wave * nranks;
+  const u32 per = (nranks + kBlock - 1) / kBlock;  // <= kPipeRPT
+  const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
+  const u32 q0 = wave * kSub + lane;
+  PhaseClock<PROF> pc(prof);
+  for (u32 r = threadIdx.x; r < nranks; r += kBlock) bse[r] = (u32)ts.base[r];  // read in B, after a barrier
+  RegReader<2> kr[kStKPL];
+  u32 cnt[kPipeRPT], chk[kPipeRPT];  // counts / chunk-prefix rows of my ranks (summed in B)
+  auto fetch = [&](u64 t) {
+    const u64 tb = t * kStTile;
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g) load_key_regs<8, true>(keys, min(tb + q0 + g * 64, n - 1), kr[g]);
+    const u32 *crow = ts.counts + t * nranks;
+    const u32 *hrow = ts.chunks + (t / kBucketChunk) * nranks;
+#pragma unroll
+    for (u32 k = 0; k < kPipeRPT; ++k) {
+      const u32 r = min(rb0 + k, nranks - 1);
+      cnt[k] = crow[r];
+      chk[k] = hrow[r];
+    }
+  };
+  TileOrder o(ntiles);
+  if (o.t < o.end) fetch(o.t);
+  // Drain the first fetch here (compiler-visible wait): the loop header then
+  // sees loads pending only from the back edge, where the stores follow them,
+  // and its key waits become vmcnt(<= 63) instead of vmcnt(15).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  for (; o.t < o.end; o.t += o.step) {
+    const u64 t = o.t;
+    const u64 tbase = t * kStTile;
+    const u32 tn = (u32)min((u64)kStTile, n - tbase);
+    pc.tile();
+    for (u32 j = threadIdx.x; j < kStW * nranks; j += kBlock) run[j] = 0;
+    u64 h[kStKPL];
+    u32 rr[kStKPL];
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g) {
+      h[g] = city64(kr[g], (u64)8);
+      rr[g] = (u32)rk.mod(h[g]);
+    }
+    __syncthreads();
+    pc.mark(0);
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g)
+      if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
+    __syncthreads();
+    pc.mark(1);
+    u32 s = 0;
+    for (u32 r = rb0; r < rb1; ++r)
+#pragma unroll
+      for (int w = 0; w < kStW; ++w) s += run[w * nranks + r];
+    u32 acc = block_exclusive_scan<kStW>(s, scan_scratch);
+#pragma unroll
+    for (u32 k = 0; k < kPipeRPT; ++k) {
+      const u32 r = rb0 + k;
+      if (r < rb1) {
+        delta[r] = bse[r] + cnt[k] + chk[k] - acc;
+#pragma unroll
+        for (int w = 0; w < kStW; ++w) {
+          const u32 v = run[w * nranks + r];
+          run[w * nranks + r] = acc;
+          acc += v;
+        }
+      }
+    }
+    __syncthreads();
+    pc.mark(2);
+    u32 lp[kStKPL];
+    rank_groups<kStKPL>(myrun, rr, q0, tn, nbits, lp);
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g)
+      if (q0 + g * 64 < tn) {
+        stage[lp[g]] = h[g];
+        sidx[lp[g]] = (uint16_t)(q0 + g * 64);
+      }
+    __syncthreads();
+    pc.mark(3);
+    u64 hv[kPer], kv[kPer];
+    u32 gp[kPer], si[kPer];
+    // entries past a partial tile's end repeat its last entry (the same bytes
+    // to the same slots), so that every store below is unconditional: a store
+    // under a branch would let the compiler assume a path with no stores after
+    // the prefetch and wait for all of them at the next tile's first key
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 jc = min(jj * kBlock + threadIdx.x, tn - 1);
+      hv[jj] = stage[jc];
+      si[jj] = sidx[jc];
+      gp[jj] = delta[(u32)rk.mod(hv[jj])] + jc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < kStKPL; ++g)
+      if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) kv[jj] = stage[min(jj * kBlock + threadIdx.x, tn - 1)];
+    if (o.t + o.step < o.end) fetch(o.t + o.step);
+    __builtin_amdgcn_sched_barrier(0);  // the loads above go out before the stores below
+    pc.mark(4);
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      mbits_out[gp[jj]] = hv[jj];
+      ptindex_out[gp[jj]] = (u32)pt.mod(hv[jj]);
+      index_out[gp[jj]] = tbase + si[jj];
+      reinterpret_cast<u64 *>(keys_out)[gp[jj]] = kv[jj];
+    }
+    __syncthreads();  // the staging buffer and delta are reused by the next tile
+    pc.mark(5);
+  }
+  pc.flush();
 }
 
 // ------------------------------------------- register scatter (no staging) ---

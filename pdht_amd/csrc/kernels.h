@@ -383,15 +383,17 @@ __device__ __forceinline__ void load_key_regs(const uint8_t *__restrict__ keys, 
   }}
 
 // ------------------------------------------------------- direct kernel ---
-// U keys per lane per iteration (all loads issued before any hashing).
-template <int L, int U, class Algo, class Sink, bool NT = false>
-__global__ __launch_bounds__(kBlock) void k_fixed_direct(const uint8_t *__restrict__ keys, u64 n,
-                                                         Algo algo, Sink sink) {
+// U keys per lane per iteration (all loads issued before any hashing).  BS =
+// workgroup size: fused placement with a histogram uses 1024 so that a quarter
+// as many workgroups flush their LDS bins with device-scope atomics.
+template <int L, int U, class Algo, class Sink, bool NT = false, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_fixed_direct(const uint8_t *__restrict__ keys, u64 n,
+                                                     Algo algo, Sink sink) {
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
   sink.init();
-  const u64 stride = (u64)gridDim.x * kBlock;
-  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride * U) {
+  const u64 stride = (u64)gridDim.x * BS;
+  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n; i += stride * U) {
     RegReader<L / 4> r[U];
     // unconditional (clamped) loads: a load under a lane-divergent branch is
     // followed by its own vmcnt(0), which would serialise the U keys

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/pdht_hip.h"
@@ -100,6 +101,31 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
                          hipStream_t st, int dev, u64 blocks, int variant) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt snt = NtSink<Sink>::make(sink);
+  if constexpr (std::is_same<Sink, SinkPlace>::value) {
+    // With a histogram: 1024-thread workgroups, 2 per CU.  Every workgroup
+    // flushes its LDS bins with one device-scope atomic per bin, and those
+    // run at the memory-side atomic rate (~1.3 TB/s of added bytes): 2048
+    // workgroups x 1024 bins x 8 B took ~16 us of an 85-us launch; a quarter
+    // as many workgroups measured +24 % (8-B keys) and +29 % (16-B keys) on
+    // 16M keys, 1024 ranks (tools/placebench.py, r01).  Variant 20 keeps the
+    // 256-thread kernel; 19 forces this one.
+    const bool wide = variant == 19 || (sink.hist && variant != 16 && variant != 17 && variant != 18 &&
+                                        variant != 20);
+    if (wide) {
+      if (keylen == 8) {
+        g_kernel = "k_fixed_direct<8,4,nt-store,1024>";
+        k_fixed_direct<8, 4, Algo, SinkNt, false, 1024>
+            <<<grid_for((blocks + 15) / 16, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+        return;
+      }
+      if (keylen == 16) {
+        g_kernel = "k_fixed_direct<16,2,nt,1024>";
+        k_fixed_direct<16, 2, Algo, SinkNt, true, 1024>
+            <<<grid_for((blocks + 7) / 8, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+        return;
+      }
+    }
+  }
   if constexpr (LMAX == 8) {
     const unsigned g = grid_for((blocks + 3) / 4, 8, dev);
     if (variant == 16) {
@@ -852,6 +878,7 @@ PDHT_API int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
 
 // ------------------------------------------------- destination bucketing ---
 namespace pdht {
+static u64 *g_phase = nullptr;  // pdht_hip_set_phase_counters (tuning only)
 struct BucketWs {
   u32 *counts, *chunks;
   u64 *totals, *base;
@@ -896,17 +923,36 @@ struct BucketArgs {
   u64 *ix;
 };
 
-template <int L>
+// SERIAL: one group at a time in the tile-local ranking (variant 41, the r01
+// kernel) instead of the batched LDS atomics (rank_groups).
+template <int L, bool SERIAL = false, int DBG = 0>
 static int launch_staged(const BucketArgs &a, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
-  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  static const char *const serial_names[3] = {"k_bucket_scatter_staged<8B,serial-rank>",
+                                              "k_bucket_scatter_staged<16B,serial-rank>",
+                                              "k_bucket_scatter_staged<32B,serial-rank>"};
+  g_kernel = (SERIAL ? serial_names : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
   const size_t bytes = staged_lds_bytes(a.nranks);
-  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_staged<L>), bytes)) return rc;
+  // the phase-clock build only while pdht_hip_set_phase_counters is active
+  auto fn = g_phase ? &k_bucket_scatter_staged<L, !SERIAL, DBG, true> : &k_bucket_scatter_staged<L, !SERIAL, DBG>;
+  if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
   unsigned g = grid_for(a.ntiles, bytes <= 80 * 1024 ? 2 : 1, dev);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-  k_bucket_scatter_staged<L><<<g, kBlock, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts,
-                                                      a.ntiles, a.ko, a.mb, a.pi, a.ix);
+  fn<<<g, kBlock, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi,
+                               a.ix, g_phase);
+  return 0;
+}
+
+static int launch_pipe8(const BucketArgs &a, hipStream_t st, int dev) {
+  g_kernel = "k_bucket_scatter_pipe<8B>";
+  const size_t bytes = pipe_lds_bytes(a.nranks);
+  auto fn = g_phase ? &k_bucket_scatter_pipe8<true> : &k_bucket_scatter_pipe8<false>;
+  if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
+  unsigned g = grid_for(a.ntiles, bytes <= 80 * 1024 ? 2 : 1, dev);
+  if (g >= 8) g &= ~7u;
+  fn<<<g, kBlock, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi, a.ix,
+                               g_phase);
   return 0;
 }
 
@@ -934,6 +980,11 @@ static int launch_wg(const BucketArgs &a, u32 L, hipStream_t st, int dev) {
 
 enum class BucketKernel { kStaged, kReg, kGeneric };
 }  // namespace pdht
+
+PDHT_API int pdht_hip_set_phase_counters(uint64_t *buf) {
+  g_phase = buf;
+  return 0;
+}
 
 PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
   return bucket_layout(nullptr, n, nranks).bytes;
@@ -1006,7 +1057,21 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
-    if (kind == BucketKernel::kStaged)
+    if (kind == BucketKernel::kStaged && keysize == 8 && variant == 40 && a.ko && a.pi && a.ix)
+      rc = launch_pipe8(a, st, dev);
+    else if (kind == BucketKernel::kStaged && variant == 41)
+      rc = keysize == 8    ? launch_staged<8, true>(a, st, dev)
+           : keysize == 16 ? launch_staged<16, true>(a, st, dev)
+                           : launch_staged<32, true>(a, st, dev);
+    else if (kind == BucketKernel::kStaged && keysize == 8 && variant >= 50 && variant <= 55)
+      // timing-only builds (wrong results): the r01 kernel with parts removed
+      rc = variant == 50   ? launch_staged<8, true, 1>(a, st, dev)
+           : variant == 51 ? launch_staged<8, true, 2>(a, st, dev)
+           : variant == 52 ? launch_staged<8, true, 4>(a, st, dev)
+           : variant == 53 ? launch_staged<8, true, 8>(a, st, dev)
+           : variant == 54 ? launch_staged<8, true, 12>(a, st, dev)
+                           : launch_staged<8, true, 15>(a, st, dev);
+    else if (kind == BucketKernel::kStaged)
       rc = keysize == 8    ? launch_staged<8>(a, st, dev)
            : keysize == 16 ? launch_staged<16>(a, st, dev)
                            : launch_staged<32>(a, st, dev);

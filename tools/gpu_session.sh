@@ -50,6 +50,8 @@ for step in "$@"; do
              tail -1 gpurun_out/torchrun1.log | cut -c1-400 ;;
     placebench) timeout -k 10 300 python tools/placebench.py --variants ${PVARIANTS:-0,16,17} > gpurun_out/placebench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/placebench.log | cut -c1-220 ;;
+    bucketbench) timeout -k 10 300 python tools/bucketbench.py --variants ${BVARIANTS:-0,40} ${BARGS:-} >> gpurun_out/bucketbench.log 2>&1; rc=$?
+             grep -v amdgpu.ids gpurun_out/bucketbench.log | cut -c1-400 ;;
     counters) timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; rc=$?; rc=0 ;;
     sq_*)    cfg=${step#sq_}
              timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sq_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/sq_$cfg.log 2>&1; rc=$?
