@@ -331,62 +331,64 @@ struct PhaseClock {
 // 8-45 % slower than this one on 16M x 8-B keys, 1024 ranks.
 constexpr int kStW = 4, kStKPL = 16;
 constexpr u32 kStTile = kStW * kStKPL * 64;
-constexpr size_t staged_lds_bytes(u32 nranks) {
-  return (size_t)kStTile * 8 + (size_t)kStTile * 2 + (size_t)kStW * nranks * 4 + (size_t)nranks * 4;
+constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL) {
+  return (size_t)W * KPL * 64 * 10 + (size_t)W * nranks * 4 + (size_t)nranks * 4;
 }
 // DBG (timing-only builds, tools/bucketbench.py; results are wrong): bit 0 =
 // identity ranking, 1 = no staging writes, 2 = no mbits/ptindex/index stores,
 // 3 = no key stores.
-template <int L, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false>
-__global__ __launch_bounds__(kStW * 64, L == 8 ? 2 : 1) void k_bucket_scatter_staged(
+// W waves x KPL groups per tile (default 4 x 16 = 4096 keys).
+template <int L, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false, int W = kStW, int KPL = kStKPL>
+__global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
     TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
     u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out, u64 *__restrict__ prof) {
+  constexpr u32 kTile = W * KPL * 64, kB = W * 64;
   extern __shared__ u64 lds64[];
-  u64 *stage = lds64;                                              // [kStTile]
-  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kStTile);  // [kStTile]
-  u32 *run = reinterpret_cast<u32 *>(sidx + kStTile);              // [kStW][nranks]
-  u32 *delta = run + kStW * nranks;                                // [nranks]
-  __shared__ u32 scan_scratch[kStW];
-  constexpr u32 kSub = kStKPL * 64;
+  u64 *stage = lds64;                                              // [kTile]
+  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile]
+  u32 *run = reinterpret_cast<u32 *>(sidx + kTile);              // [W][nranks]
+  u32 *delta = run + W * nranks;                                // [nranks]
+  __shared__ u32 scan_scratch[W];
+  constexpr u32 kSub = KPL * 64;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   u32 *myrun = run + wave * nranks;
-  const u32 per = (nranks + kBlock - 1) / kBlock;
+  const u32 per = (nranks + kB - 1) / kB;
   const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
   PhaseClock<PROF> pc(prof);
   for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
     const u64 t = o.t;
-    const u64 tbase = t * kStTile;
-    const u32 tn = (u32)min((u64)kStTile, n - tbase);
+    const u64 tbase = t * kTile;
+    const u32 tn = (u32)min((u64)kTile, n - tbase);
     pc.tile();
-    for (u32 j = threadIdx.x; j < kStW * nranks; j += kBlock) run[j] = 0;
+    for (u32 j = threadIdx.x; j < W * nranks; j += kB) run[j] = 0;
     const u32 q0 = wave * kSub + lane;
-    RegReader<L / 4> kr[kStKPL];
+    RegReader<L / 4> kr[KPL];
 #pragma unroll
-    for (int g = 0; g < kStKPL; ++g) load_key_regs<L, true>(keys, min(tbase + q0 + g * 64, n - 1), kr[g]);
-    u64 h[kStKPL];
-    u32 rr[kStKPL];
+    for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(tbase + q0 + g * 64, n - 1), kr[g]);
+    u64 h[KPL];
+    u32 rr[KPL];
 #pragma unroll
-    for (int g = 0; g < kStKPL; ++g) {
+    for (int g = 0; g < KPL; ++g) {
       h[g] = city64(kr[g], (u64)L);
       rr[g] = (u32)rk.mod(h[g]);
     }
     __syncthreads();
     pc.mark(0);
 #pragma unroll
-    for (int g = 0; g < kStKPL; ++g)
+    for (int g = 0; g < KPL; ++g)
       if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
     __syncthreads();
     pc.mark(1);
     u32 s = 0;
     for (u32 r = rb0; r < rb1; ++r)
 #pragma unroll
-      for (int w = 0; w < kStW; ++w) s += run[w * nranks + r];
-    u32 acc = block_exclusive_scan<kStW>(s, scan_scratch);
+      for (int w = 0; w < W; ++w) s += run[w * nranks + r];
+    u32 acc = block_exclusive_scan<W>(s, scan_scratch);
     for (u32 r = rb0; r < rb1; ++r) {
       delta[r] = ts.at(r, t) - acc;
 #pragma unroll
-      for (int w = 0; w < kStW; ++w) {
+      for (int w = 0; w < W; ++w) {
         const u32 v = run[w * nranks + r];
         run[w * nranks + r] = acc;
         acc += v;
@@ -394,28 +396,28 @@ __global__ __launch_bounds__(kStW * 64, L == 8 ? 2 : 1) void k_bucket_scatter_st
     }
     __syncthreads();
     pc.mark(2);
-    u32 lp[kStKPL];
+    u32 lp[KPL];
     if constexpr (DBG & 1) {
 #pragma unroll
-      for (int g = 0; g < kStKPL; ++g) lp[g] = q0 + g * 64;
+      for (int g = 0; g < KPL; ++g) lp[g] = q0 + g * 64;
     } else if constexpr (BATCHED_RANK) {
-      rank_groups<kStKPL>(myrun, rr, q0, tn, nbits, lp);
+      rank_groups<KPL>(myrun, rr, q0, tn, nbits, lp);
     } else {
-      rank_groups_serial<kStKPL>(myrun, rr, q0, tn, nbits, lp);
+      rank_groups_serial<KPL>(myrun, rr, q0, tn, nbits, lp);
     }
 #pragma unroll
-    for (int g = 0; g < kStKPL; ++g)
+    for (int g = 0; g < KPL; ++g)
       if (!(DBG & 2) && q0 + g * 64 < tn) {
         stage[lp[g]] = h[g];
         sidx[lp[g]] = (uint16_t)(q0 + g * 64);
       }
     __syncthreads();
     pc.mark(3);
-    constexpr int kPer = kStTile / kBlock;
+    constexpr int kPer = kTile / kB;
     u32 gp[kPer];
 #pragma unroll
     for (int jj = 0; jj < kPer; ++jj) {
-      const u32 j = jj * kBlock + threadIdx.x;
+      const u32 j = jj * kB + threadIdx.x;
       if (j < tn) {
         const u64 hv = stage[j];
         gp[jj] = delta[(u32)rk.mod(hv)] + j;
@@ -430,161 +432,18 @@ __global__ __launch_bounds__(kStW * 64, L == 8 ? 2 : 1) void k_bucket_scatter_st
       for (int c = 0; c < L / 8; ++c) {
         __syncthreads();
 #pragma unroll
-        for (int g = 0; g < kStKPL; ++g)
+        for (int g = 0; g < KPL; ++g)
           if (q0 + g * 64 < tn)
             stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
         __syncthreads();
 #pragma unroll
         for (int jj = 0; jj < kPer; ++jj) {
-          const u32 j = jj * kBlock + threadIdx.x;
+          const u32 j = jj * kB + threadIdx.x;
           if (j < tn) *reinterpret_cast<u64 *>(keys_out + (u64)gp[jj] * L + c * 8) = stage[j];
         }
       }
     }
     __syncthreads();
-    pc.mark(5);
-  }
-  pc.flush();
-}
-
-// ------------------------------------------------ pipelined staged scatter ---
-// 8-B keys.  The staged scatter's phases, reordered so that no load waits for
-// this tile's stores: on gfx9 vmcnt retires in issue order, so a load wait
-// also waits for every store issued before the load.  Per tile:
-//   A/B/C as in _staged, with the tile starts (counts + chunk prefix rows,
-//         loaded with the keys) and the bucket bases (constant, loaded once)
-//         already in registers;
-//   D: each thread gathers its 16 staged digests, indices and -- through the
-//      same buffer -- keys into registers, computing the global slots;
-//   P: the NEXT tile's keys and tile starts are issued;
-//   S: all stores of this tile (mbits, ptindex, index, keys) from registers.
-// The loads of P retire before the stores of S, so the next tile's first
-// wait covers only them.  Needs every output (keys, ptindex, index).
-constexpr u32 kPipeRPT = kStagedMaxRanks / kBlock;  // ranks per thread (8)
-constexpr size_t pipe_lds_bytes(u32 nranks) { return staged_lds_bytes(nranks) + (size_t)nranks * 4; }
-template <bool PROF = false>
-__global__ __launch_bounds__(kStW * 64, 2) void k_bucket_scatter_pipe8(
-    const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
-    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
-    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out, u64 *__restrict__ prof) {
-  extern __shared__ u64 lds64[];
-  u64 *stage = lds64;                                              // [kStTile]
-  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kStTile);  // [kStTile]
-  u32 *run = reinterpret_cast<u32 *>(sidx + kStTile);              // [kStW][nranks]
-  u32 *delta = run + kStW * nranks;                                // [nranks]
-  u32 *bse = delta + nranks;  // [nranks] low words of the bucket bases (slots < 2^32)
-  __shared__ u32 scan_scratch[kStW];
-  constexpr u32 kSub = kStKPL * 64;
-  constexpr int kPer = kStTile / kBlock;
-  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  u32 *myrun = run + wave * nranks;
-  const u32 per = (nranks + kBlock - 1) / kBlock;  // <= kPipeRPT
-  const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
-  const u32 q0 = wave * kSub + lane;
-  PhaseClock<PROF> pc(prof);
-  for (u32 r = threadIdx.x; r < nranks; r += kBlock) bse[r] = (u32)ts.base[r];  // read in B, after a barrier
-  RegReader<2> kr[kStKPL];
-  u32 cnt[kPipeRPT], chk[kPipeRPT];  // counts / chunk-prefix rows of my ranks (summed in B)
-  auto fetch = [&](u64 t) {
-    const u64 tb = t * kStTile;
-#pragma unroll
-    for (int g = 0; g < kStKPL; ++g) load_key_regs<8, true>(keys, min(tb + q0 + g * 64, n - 1), kr[g]);
-    const u32 *crow = ts.counts + t * nranks;
-    const u32 *hrow = ts.chunks + (t / kBucketChunk) * nranks;
-#pragma unroll
-    for (u32 k = 0; k < kPipeRPT; ++k) {
-      const u32 r = min(rb0 + k, nranks - 1);
-      cnt[k] = crow[r];
-      chk[k] = hrow[r];
-    }
-  };
-  TileOrder o(ntiles);
-  if (o.t < o.end) fetch(o.t);
-  // Drain the first fetch here (compiler-visible wait): the loop header then
-  // sees loads pending only from the back edge, where the stores follow them,
-  // and its key waits become vmcnt(<= 63) instead of vmcnt(15).
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-  for (; o.t < o.end; o.t += o.step) {
-    const u64 t = o.t;
-    const u64 tbase = t * kStTile;
-    const u32 tn = (u32)min((u64)kStTile, n - tbase);
-    pc.tile();
-    for (u32 j = threadIdx.x; j < kStW * nranks; j += kBlock) run[j] = 0;
-    u64 h[kStKPL];
-    u32 rr[kStKPL];
-#pragma unroll
-    for (int g = 0; g < kStKPL; ++g) {
-      h[g] = city64(kr[g], (u64)8);
-      rr[g] = (u32)rk.mod(h[g]);
-    }
-    __syncthreads();
-    pc.mark(0);
-#pragma unroll
-    for (int g = 0; g < kStKPL; ++g)
-      if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
-    __syncthreads();
-    pc.mark(1);
-    u32 s = 0;
-    for (u32 r = rb0; r < rb1; ++r)
-#pragma unroll
-      for (int w = 0; w < kStW; ++w) s += run[w * nranks + r];
-    u32 acc = block_exclusive_scan<kStW>(s, scan_scratch);
-#pragma unroll
-    for (u32 k = 0; k < kPipeRPT; ++k) {
-      const u32 r = rb0 + k;
-      if (r < rb1) {
-        delta[r] = bse[r] + cnt[k] + chk[k] - acc;
-#pragma unroll
-        for (int w = 0; w < kStW; ++w) {
-          const u32 v = run[w * nranks + r];
-          run[w * nranks + r] = acc;
-          acc += v;
-        }
-      }
-    }
-    __syncthreads();
-    pc.mark(2);
-    u32 lp[kStKPL];
-    rank_groups<kStKPL>(myrun, rr, q0, tn, nbits, lp);
-#pragma unroll
-    for (int g = 0; g < kStKPL; ++g)
-      if (q0 + g * 64 < tn) {
-        stage[lp[g]] = h[g];
-        sidx[lp[g]] = (uint16_t)(q0 + g * 64);
-      }
-    __syncthreads();
-    pc.mark(3);
-    u64 hv[kPer], kv[kPer];
-    u32 gp[kPer], si[kPer];
-    // entries past a partial tile's end repeat its last entry (the same bytes
-    // to the same slots), so that every store below is unconditional: a store
-    // under a branch would let the compiler assume a path with no stores after
-    // the prefetch and wait for all of them at the next tile's first key
-#pragma unroll
-    for (int jj = 0; jj < kPer; ++jj) {
-      const u32 jc = min(jj * kBlock + threadIdx.x, tn - 1);
-      hv[jj] = stage[jc];
-      si[jj] = sidx[jc];
-      gp[jj] = delta[(u32)rk.mod(hv[jj])] + jc;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < kStKPL; ++g)
-      if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
-    __syncthreads();
-#pragma unroll
-    for (int jj = 0; jj < kPer; ++jj) kv[jj] = stage[min(jj * kBlock + threadIdx.x, tn - 1)];
-    if (o.t + o.step < o.end) fetch(o.t + o.step);
-    __builtin_amdgcn_sched_barrier(0);  // the loads above go out before the stores below
-    pc.mark(4);
-#pragma unroll
-    for (int jj = 0; jj < kPer; ++jj) {
-      mbits_out[gp[jj]] = hv[jj];
-      ptindex_out[gp[jj]] = (u32)pt.mod(hv[jj]);
-      index_out[gp[jj]] = tbase + si[jj];
-      reinterpret_cast<u64 *>(keys_out)[gp[jj]] = kv[jj];
-    }
-    __syncthreads();  // the staging buffer and delta are reused by the next tile
     pc.mark(5);
   }
   pc.flush();

@@ -925,34 +925,26 @@ struct BucketArgs {
 
 // SERIAL: one group at a time in the tile-local ranking (variant 41, the r01
 // kernel) instead of the batched LDS atomics (rank_groups).
-template <int L, bool SERIAL = false, int DBG = 0>
+template <int L, bool SERIAL = false, int DBG = 0, int W = kStW, int KPL = kStKPL>
 static int launch_staged(const BucketArgs &a, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
   static const char *const serial_names[3] = {"k_bucket_scatter_staged<8B,serial-rank>",
                                               "k_bucket_scatter_staged<16B,serial-rank>",
                                               "k_bucket_scatter_staged<32B,serial-rank>"};
-  g_kernel = (SERIAL ? serial_names : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
-  const size_t bytes = staged_lds_bytes(a.nranks);
+  static const char *const wide_names[3] = {"k_bucket_scatter_staged<8B,8x16>", "k_bucket_scatter_staged<16B,8x16>",
+                                            "k_bucket_scatter_staged<32B,8x16>"};
+  g_kernel = (W == 8 ? wide_names : SERIAL ? serial_names : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = staged_lds_bytes(a.nranks, W, KPL);
   // the phase-clock build only while pdht_hip_set_phase_counters is active
-  auto fn = g_phase ? &k_bucket_scatter_staged<L, !SERIAL, DBG, true> : &k_bucket_scatter_staged<L, !SERIAL, DBG>;
+  auto fn = g_phase ? &k_bucket_scatter_staged<L, !SERIAL, DBG, true, W, KPL>
+                    : &k_bucket_scatter_staged<L, !SERIAL, DBG, false, W, KPL>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
-  unsigned g = grid_for(a.ntiles, bytes <= 80 * 1024 ? 2 : 1, dev);
+  const int per_cu = env_int("PDHT_HIP_SCATTER_PER_CU", bytes <= 80 * 1024 ? 2 : 1);  // tuning only
+  unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-  fn<<<g, kBlock, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi,
+  fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi,
                                a.ix, g_phase);
-  return 0;
-}
-
-static int launch_pipe8(const BucketArgs &a, hipStream_t st, int dev) {
-  g_kernel = "k_bucket_scatter_pipe<8B>";
-  const size_t bytes = pipe_lds_bytes(a.nranks);
-  auto fn = g_phase ? &k_bucket_scatter_pipe8<true> : &k_bucket_scatter_pipe8<false>;
-  if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
-  unsigned g = grid_for(a.ntiles, bytes <= 80 * 1024 ? 2 : 1, dev);
-  if (g >= 8) g &= ~7u;
-  fn<<<g, kBlock, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi, a.ix,
-                               g_phase);
   return 0;
 }
 
@@ -978,7 +970,7 @@ static int launch_wg(const BucketArgs &a, u32 L, hipStream_t st, int dev) {
   return 0;
 }
 
-enum class BucketKernel { kStaged, kReg, kGeneric };
+enum class BucketKernel { kStaged, kStagedWide, kReg, kGeneric };
 }  // namespace pdht
 
 PDHT_API int pdht_hip_set_phase_counters(uint64_t *buf) {
@@ -1007,16 +999,19 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
   hipStream_t st = ST(s);
   // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter up to
   // 2048 ranks, register scatter above; other lengths -> generic.  Variants:
-  // 21 forces generic, 22 forces register.
+  // 21 forces generic, 22 register, 41 staged with group-serial ranking (r01),
+  // 43 staged with 8 waves x 8192-key tiles, 50-55 timing-only staged builds.
   const int variant = g_variant.load(std::memory_order_relaxed);
   const uintptr_t al = (uintptr_t)keys | (uintptr_t)keys_out;
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
-  BucketKernel kind = !fixed || variant == 21        ? BucketKernel::kGeneric
+  BucketKernel kind = !fixed || variant == 21                   ? BucketKernel::kGeneric
                       : variant == 22 || nranks > kStagedMaxRanks ? BucketKernel::kReg
-                                                               : BucketKernel::kStaged;
+                      : variant == 43                             ? BucketKernel::kStagedWide
+                                                                  : BucketKernel::kStaged;
   const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
   const int reg_kpl = keysize == 32 ? 8 : 16;
-  const u64 tile = kind == BucketKernel::kStaged ? kStTile
+  const u64 tile = kind == BucketKernel::kStaged    ? kStTile
+                   : kind == BucketKernel::kStagedWide ? (u64)8 * kStKPL * 64
                    : kind == BucketKernel::kReg  ? (u64)waves * reg_kpl * 64
                                                  : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
@@ -1057,8 +1052,10 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
-    if (kind == BucketKernel::kStaged && keysize == 8 && variant == 40 && a.ko && a.pi && a.ix)
-      rc = launch_pipe8(a, st, dev);
+    if (kind == BucketKernel::kStagedWide)
+      rc = keysize == 8    ? launch_staged<8, false, 0, 8, kStKPL>(a, st, dev)
+           : keysize == 16 ? launch_staged<16, false, 0, 8, kStKPL>(a, st, dev)
+                           : launch_staged<32, false, 0, 8, kStKPL>(a, st, dev);
     else if (kind == BucketKernel::kStaged && variant == 41)
       rc = keysize == 8    ? launch_staged<8, true>(a, st, dev)
            : keysize == 16 ? launch_staged<16, true>(a, st, dev)

@@ -3,7 +3,7 @@
 packed keys, kernel variants interleaved in one process, plus the per-phase
 shader-clock split of the scatter kernel (pdht_hip_set_phase_counters).
 
-  python tools/bucketbench.py [--n 16777216] [--L 8] [--nranks 1024] [--variants 0,40]
+  python tools/bucketbench.py [--n 16777216] [--L 8] [--nranks 1024] [--variants 0,41]
 """
 import argparse
 import json
@@ -37,11 +37,24 @@ def main():
     ap.add_argument("--nranks", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="0,40")
+    ap.add_argument("--variants", default="0,41")
+    ap.add_argument("--per-cu", default="", help="comma list of PDHT_HIP_SCATTER_PER_CU values to sweep")
     a = ap.parse_args()
+    if a.per_cu:  # each (variant, blocks per CU) pair becomes its own case
+        pcs = [int(x) for x in a.per_cu.split(",")]
+        a.variants = ",".join(f"{v}@{p}" for v in a.variants.split(",") for p in pcs)
     dev = torch.device("cuda:0")
     n, L, nr = a.n, a.L, a.nranks
-    variants = [int(x) for x in a.variants.split(",")]
+    variants = a.variants.split(",")
+
+    def use(v):
+        """'v' or 'v@blocks_per_cu'"""
+        var, _, pc = v.partition("@")
+        P.set_variant(int(var))
+        if pc:
+            os.environ["PDHT_HIP_SCATTER_PER_CU"] = pc
+        else:
+            os.environ.pop("PDHT_HIP_SCATTER_PER_CU", None)
     w = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, n * L // 8, device=dev)
     keys = w.view(torch.uint8).view(n, L)
     ws = torch.empty(P.bucket_workspace_bytes(n, nr), dtype=torch.uint8, device=dev)
@@ -51,7 +64,7 @@ def main():
     ms = {v: [] for v in variants}
     kern, ref = {}, None
     for v in variants:
-        P.set_variant(v)
+        use(v)
         fn()
         kern[v] = P.last_kernel()
         got = [t.clone() for t in outs]
@@ -61,10 +74,10 @@ def main():
             print(json.dumps({"variant": v, "error": "output differs from the first variant"}), flush=True)
     for _ in range(a.rounds):
         for v in variants:
-            P.set_variant(v)
+            use(v)
             ms[v].extend(timeit(fn, a.reps))
     for v in variants:
-        P.set_variant(v)
+        use(v)
         ctr = torch.zeros(16, dtype=torch.int64, device=dev)
         P.set_phase_counters(ctr)
         try:
@@ -82,7 +95,7 @@ def main():
                           "cycles_per_tile": round(tot / max(1, int(c[8])), 1),
                           "phase_share": {p: round(int(c[k]) / tot, 3) for k, p in enumerate(PHASES)}}),
               flush=True)
-    P.set_variant(0)
+    use("0")
 
 
 if __name__ == "__main__":

@@ -50,7 +50,7 @@ for step in "$@"; do
              tail -1 gpurun_out/torchrun1.log | cut -c1-400 ;;
     placebench) timeout -k 10 300 python tools/placebench.py --variants ${PVARIANTS:-0,16,17} > gpurun_out/placebench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/placebench.log | cut -c1-220 ;;
-    bucketbench) timeout -k 10 300 python tools/bucketbench.py --variants ${BVARIANTS:-0,40} ${BARGS:-} >> gpurun_out/bucketbench.log 2>&1; rc=$?
+    bucketbench) timeout -k 10 300 python tools/bucketbench.py --variants ${BVARIANTS:-0,41} ${BARGS:-} >> gpurun_out/bucketbench.log 2>&1; rc=$?
              grep -v amdgpu.ids gpurun_out/bucketbench.log | cut -c1-400 ;;
     counters) timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; rc=$?; rc=0 ;;
     sq_*)    cfg=${step#sq_}
