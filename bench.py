@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident batch CityHash64 on 64-byte keys (BASELINE.json).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5|place]
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+                  [--config cfg2|cfg3|cfg4|cfg5|place|bucket|exchange|records|xrecords|long]
 
 One step = one pass of the hot path (one kernel launch) over this GPU's batch
 of synthetic keys already resident in HBM.  Default workload = BASELINE
@@ -56,7 +57,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange", "long"])
+                    choices=["cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange", "records",
+                             "xrecords", "long"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (tools/kbench.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -99,7 +101,31 @@ def main():
     # ---------------------------------------------------------- workload ---
     keys = out = data = offs = None
     bucketed = None
-    if cfg in ("bucket", "exchange"):
+    if cfg in ("records", "xrecords"):
+        # f4 in the MPI wire format: one message_t record (header + key) per
+        # key at its bucketed position; "xrecords" buckets by the world size
+        # and ships every bucket to its owner in ONE all-to-all(v) (RCCL)
+        L = 8
+        n = a.keys_per_gpu or 16 * M
+        sh = D.weak_shard(rank, world, n)
+        words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
+        keys = words.view(torch.uint8).view(n, L)
+        nr = 1024 if cfg == "records" else world
+        ws = torch.empty(P.bucket_workspace_bytes(n, nr), dtype=torch.uint8, device=dev)
+        recs = P.bucket_records(keys, nr, src_rank=rank, workspace=ws)
+        bucketed = {"nranks": nr, "records": True}
+
+        def step():
+            rec, offs_ = P.bucket_records(keys, nr, src_rank=rank, out=recs, workspace=ws)
+            bucketed.update(rec=rec, offs=offs_)
+            if cfg == "xrecords" and world > 1:
+                bucketed["x"] = D.exchange_records(rec, offs_)
+        out = None
+        bytes_per_key = L + P.bucket_record_bytes(L)
+        workload = (f"{cfg}: destination bucketing of {n >> 20}M x 8B keys per GPU by CityHash64 % {nr} into "
+                    f"message_t wire records" + (" + all-to-all(v) exchange" if cfg == "xrecords" else ""))
+        total_bytes_in = n * L
+    elif cfg in ("bucket", "exchange"):
         # f4: stable counting sort of 8-B keys by destination rank (keys, mbits,
         # ptindex, original index written at bucketed positions); "exchange"
         # buckets by the world size and ships each bucket to its owner with
@@ -243,7 +269,9 @@ def main():
         del fold
 
     # ------------------------------------------------------------ parity ---
-    if bucketed is not None:
+    if bucketed is not None and bucketed.get("records"):
+        parity = check_records(P, torch, D, sh, keys, bucketed, dev)
+    elif bucketed is not None:
         parity = check_buckets(P, torch, D, sh, keys, bucketed, dev)
     else:
         extra = None
@@ -412,6 +440,54 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
             want = P.splitmix64_fill(SEED_KEYS, int(xi[j].item()), 1, device=dev)
             mine = mine and bool((xk[j].view(torch.int64) == want).all().item())
         msgs.append(f"exchange: {xi.numel()} keys received, all owned by this rank {'ok' if mine else 'FAILED'}")
+        ok = ok and mine
+    all_ok = D.allreduce_min_flag(ok, device=dev)
+    if sh.world > 1:
+        msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
+    return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
+
+
+def check_records(P, torch, D, sh, keys, b, dev):
+    """Record bucketing checks without oracle code: the records' mbits and
+    source-index columns and the bucket offsets against the same reference
+    golden folds as the array form (bucket config), and full-size properties:
+    index is a permutation, buckets are stable, every record's key and mbits
+    agree with the keys at its source index and with CityHash64 of its key."""
+    nr, rec, offs = b["nranks"], b["rec"], b["offs"]
+    n = rec.shape[0]
+    ty, sr, hi, ix32, mb, ko = P.record_fields(rec, keys.shape[1])
+    ix = ix32.to(torch.int64) & 0xFFFFFFFF
+    msgs, ok = [], True
+    g = (golden_folds() or {}).get("bucket_8B_16M", {})
+    r = sh.first // (16 * M)
+    if nr == g.get("nranks") and n == g.get("n") and sh.first % n == 0 and r < len(g.get("shards", [])):
+        gs = g["shards"][r]
+        got = {"mbits": D.fold_tensor(mb, 0), "index": D.fold_tensor(ix, 0), "offsets": D.fold_tensor(offs, 0)}
+        bad = [k for k, v in got.items() if v != int(gs[k], 16)]
+        ok = not bad
+        msgs.append(f"records' mbits, index and offsets folds {'==' if ok else '!='} reference golden "
+                    f"(bucket shard {r})" + (f" (mismatch: {bad})" if bad else ""))
+    perm = bool((torch.sort(ix).values == torch.arange(n, device=dev)).all().item())
+    same = bool((ko == keys[ix]).all().item()) and bool((P.city64_batch(ko.contiguous()) == mb).all().item())
+    hdr = bool(((ty == P.PDHT_PUT) & (sr == sh.rank) & (hi == 0)).all().item())
+    cnt = offs[1:] - offs[:-1]
+    rk = torch.repeat_interleave(torch.arange(nr, device=dev), cnt)
+    prop = perm and same and hdr and int(offs[-1].item()) == n
+    if n > 1:
+        prop = prop and bool(((ix[1:] > ix[:-1]) | (rk[1:] > rk[:-1])).all().item())
+    msgs.append(f"full batch: permutation, stable buckets, headers, keys/mbits consistent {'ok' if prop else 'FAILED'}")
+    ok = ok and prop
+    if "x" in b:
+        xr, _ = b["x"]
+        xt, xs, xh, xi, xm, xk = P.record_fields(xr, keys.shape[1])
+        got_m = xm.cpu().numpy().view(np.uint64)
+        mine = bool((got_m % np.uint64(sh.world) == np.uint64(sh.rank)).all())
+        mine = mine and bool((P.city64_batch(xk.contiguous()) == xm).all().item())
+        gidx = xs.to(torch.int64) * sh.n + (xi.to(torch.int64) & 0xFFFFFFFF)
+        for j in range(0, gidx.numel(), max(1, gidx.numel() // 256)):
+            want = P.splitmix64_fill(SEED_KEYS, int(gidx[j].item()), 1, device=dev)
+            mine = mine and bool((xk[j].contiguous().view(torch.int64) == want).all().item())
+        msgs.append(f"exchange: {xr.shape[0]} records received, all owned by this rank {'ok' if mine else 'FAILED'}")
         ok = ok and mine
     all_ok = D.allreduce_min_flag(ok, device=dev)
     if sh.world > 1:

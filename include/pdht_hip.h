@@ -117,6 +117,29 @@ int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint64_t *index_out, uint64_t *bucket_offsets,
                           pdht_hip_stream_t stream);
 
+/* The same bucketing, written as one wire record per key instead of separate
+ * arrays: the MPI variant's request message (message_t,
+ * libmpipdht/pdht.h:120-127, filled by pdht_put at libmpipdht/putget.c:85-97)
+ * with the key as payload, so that bucket r is a ready send buffer for rank
+ * r.  Record at bucketed position p, stride pdht_bucket_record_bytes(keysize)
+ * = 24 + keysize rounded up to 8:
+ *   +0  uint32 type      = msg_type (pdhtPut = 1 in the reference's enum)
+ *   +4  uint32 rank      = src_rank (the sender, c->rank)
+ *   +8  uint32 ht_index  = ht_index (the table's index, c->hts[])
+ *   +12 uint32 index     = original position of the key in the batch
+ *                          (message_t's alignment padding)
+ *   +16 uint64 mbits     = CityHash64(key)
+ *   +24 key[keysize], zero-padded to the stride.
+ * records (device, 8-byte aligned) holds n records; bucket_offsets and the
+ * workspace as for pdht_bucket_batch_dev.  ptindex is not stored (it is
+ * mbits % nptes; the MPI message carries ht_index instead). */
+size_t pdht_bucket_record_bytes(size_t keysize);
+int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n,
+                            uint32_t nranks, uint32_t msg_type, uint32_t src_rank,
+                            uint32_t ht_index, void *workspace,
+                            size_t workspace_bytes, void *records,
+                            uint64_t *bucket_offsets, pdht_hip_stream_t stream);
+
 /* ---- host-resident batches ---------------------------------------------- */
 /* Keys and digests in host memory.  Chunks are copied H2D, hashed and copied
  * back D2H on several streams so copies and kernels overlap; pinned

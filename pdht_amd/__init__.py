@@ -33,7 +33,8 @@ __all__ = [
     "city128_seed_batch", "city128_var_batch", "citycrc128_batch", "citycrc128_seed_batch",
     "citycrc128_var_batch", "place_batch", "city64_batch_host", "city64_var_batch_host",
     "citycrc128_batch_host", "place_batch_host", "splitmix64_fill", "mixed_lengths",
-    "device_count", "PdhtTable", "K2",
+    "device_count", "PdhtTable", "K2", "bucket_batch", "bucket_records", "record_fields",
+    "bucket_record_bytes", "bucket_workspace_bytes",
 ]
 
 K2 = 0x9AE16A3B2F90404F  # city.c:96 (CityHash64WithSeed's seed0)
@@ -106,6 +107,8 @@ def _declare(L):
         "pdht_hip_key_stream_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
         "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _U32]),
         "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
+        "pdht_bucket_record_bytes": (C.c_size_t, [_S]),
+        "pdht_bucket_records_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _U32, _U32, _V, _S, _V, _V, _V]),
         "CityHash64": (_U64, [_V, _S]),
         "CityHash64WithSeed": (_U64, [_V, _S, _U64]),
         "CityHash64WithSeeds": (_U64, [_V, _S, _U64, _U64]),
@@ -417,6 +420,62 @@ def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=
                                        _dptr(mb), p(pt), p(ix), _dptr(offs), _stream_ptr(stream)),
            "pdht_bucket_batch_dev")
     return ko, mb, pt, ix, offs
+
+
+PDHT_PUT = 1  # msg_type pdhtPut (libmpipdht/pdht.h:72)
+
+
+def bucket_record_bytes(keysize: int) -> int:
+    return lib().pdht_bucket_record_bytes(keysize)
+
+
+def bucket_records(keys, nranks: int, *, msg_type: int = PDHT_PUT, src_rank: int = 0, ht_index: int = 0,
+                   stream=None, out=None, workspace=None):
+    """Destination bucketing into wire records (include/pdht_hip.h
+    pdht_bucket_records_dev): the MPI variant's message_t header + key for
+    every key, bucket r = records[offsets[r]:offsets[r+1]].
+
+    Returns (records uint8 [n, pdht_bucket_record_bytes(L)], offsets int64
+    [nranks+1]); record_fields() splits them into tensors.  `out` = a previous
+    return value to reuse; `workspace` as for bucket_batch.
+    """
+    torch = _torch()
+    n, L, stride = _keys_2d(keys)
+    if stride != L:
+        raise ValueError("bucket_records needs packed keys")
+    dev = keys.device
+    rb = bucket_record_bytes(L)
+    ws_bytes = lib().pdht_bucket_workspace_bytes(n, nranks)
+    if workspace is None:
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    else:
+        ws = workspace
+        if ws.numel() * ws.element_size() < ws_bytes:
+            raise ValueError(f"workspace smaller than {ws_bytes} bytes")
+        ws_bytes = ws.numel() * ws.element_size()
+    if out is not None:
+        rec, offs = out
+    else:
+        # int64 storage keeps the records 8-byte aligned
+        rec = torch.empty(max(n * rb // 8, 1), dtype=torch.int64, device=dev).view(torch.uint8)[: n * rb]
+        rec = rec.view(n, rb)
+        offs = torch.empty(nranks + 1, dtype=torch.int64, device=dev)
+    _check(lib().pdht_bucket_records_dev(_dptr(keys), L, n, nranks, msg_type, src_rank, ht_index, _dptr(ws),
+                                         ws_bytes, _dptr(rec), _dptr(offs), _stream_ptr(stream)),
+           "pdht_bucket_records_dev")
+    return rec, offs
+
+
+def record_fields(records, keysize: int):
+    """Views of a record batch [m, stride] (uint8): (type int32[m], rank
+    int32[m], ht_index int32[m], index int32[m] (unsigned), mbits int64[m],
+    keys uint8[m, keysize])."""
+    torch = _torch()
+    m, rb = records.shape
+    flat = records.contiguous().view(-1)
+    w32 = flat.view(torch.int32).view(m, rb // 4)
+    w64 = flat.view(torch.int64).view(m, rb // 8)
+    return w32[:, 0], w32[:, 1], w32[:, 2], w32[:, 3], w64[:, 2], records[:, 24:24 + keysize]
 
 
 def splitmix64_fill(seed: int, first: int, nwords: int, out=None, device="cuda", stream=None):

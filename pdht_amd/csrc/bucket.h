@@ -282,6 +282,89 @@ __device__ __forceinline__ void store_key_row(uint8_t *dst, const RegReader<L / 
   }
 }
 
+// Copy one L-byte key row (dword pieces when both rows are 4-B aligned).
+__device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L) {
+  if ((((uintptr_t)dst | (uintptr_t)src | L) & 3) == 0) {
+    const u32 *s = reinterpret_cast<const u32 *>(src);
+    u32 *d = reinterpret_cast<u32 *>(dst);
+    for (u32 j = 0; j < L / 4; ++j) d[j] = s[j];
+  } else {
+    for (u32 j = 0; j < L; ++j) dst[j] = src[j];
+  }
+}
+
+// ------------------------------------------------------------- outputs ---
+// Where a bucketed key goes; slot = its position in the bucketed batch.
+// OutSoA (pdht_bucket_batch_dev): separate arrays, each but mbits optional.
+struct OutSoA {
+  static constexpr bool kPair8 = false;
+  uint8_t *keys;
+  u64 *mbits;
+  u32 *ptindex;
+  u64 *index;
+  FastMod pt;
+  u32 L;
+  __device__ __forceinline__ void meta(u64 slot, u64 h, u64 i) const {
+    mbits[slot] = h;
+    if (ptindex) ptindex[slot] = (u32)pt.mod(h);
+    if (index) index[slot] = i;
+  }
+  __device__ __forceinline__ bool has_keys() const { return keys != nullptr; }
+  __device__ __forceinline__ void key8(u64 slot, int c, u64 v) const {  // key bytes [8c, 8c+8)
+    *reinterpret_cast<u64 *>(keys + slot * L + 8 * c) = v;
+  }
+  template <int LL>
+  __device__ __forceinline__ void key_row(u64 slot, const RegReader<LL / 4> &k) const {
+    store_key_row<LL>(keys + slot * LL, k);
+  }
+  __device__ __forceinline__ void key_copy(u64 slot, const uint8_t *src) const {
+    copy_row(keys + slot * L, src, L);
+  }
+};
+
+// OutRec (pdht_bucket_records_dev): one wire record per key, laid out as the
+// MPI variant's request message (message_t, libmpipdht/pdht.h:120-127) with
+// the key as payload:
+//   +0 u32 type  +4 u32 rank  +8 u32 ht_index  +12 u32 source index (the
+//   struct's alignment padding)  +16 u64 mbits  +24 key[L], zero-padded to
+//   the record stride 24 + round_up(L, 8).
+// One record per key means one run per bucket and tile instead of four.
+struct OutRec {
+  static constexpr bool kPair8 = true;  // 8-B keys: 32-B records written as two 16-B halves
+  uint8_t *rec;
+  u64 stride;
+  u64 hdr;  // type | rank << 32
+  u32 ht_index;
+  u32 L;
+  __device__ __forceinline__ u64 *at(u64 slot) const { return reinterpret_cast<u64 *>(rec + slot * stride); }
+  typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+  __device__ __forceinline__ void head(u64 slot, u64 i) const {  // +0 {type, rank, ht_index, index}
+    *reinterpret_cast<u64x2 *>(at(slot)) = u64x2{hdr, ht_index | (i << 32)};
+  }
+  __device__ __forceinline__ void tail8(u64 slot, u64 h, u64 key) const {  // +16 {mbits, key}
+    *reinterpret_cast<u64x2 *>(at(slot) + 2) = u64x2{h, key};
+  }
+  __device__ __forceinline__ void meta(u64 slot, u64 h, u64 i) const {
+    u64 *p = at(slot);
+    p[0] = hdr;
+    p[1] = ht_index | (i << 32);
+    p[2] = h;
+  }
+  __device__ __forceinline__ bool has_keys() const { return true; }
+  __device__ __forceinline__ void key8(u64 slot, int c, u64 v) const { at(slot)[3 + c] = v; }
+  template <int LL>
+  __device__ __forceinline__ void key_row(u64 slot, const RegReader<LL / 4> &k) const {
+    u64 *p = at(slot) + 3;
+#pragma unroll
+    for (int c = 0; c < LL / 8; ++c) p[c] = (u64)k.d[2 * c] | ((u64)k.d[2 * c + 1] << 32);
+  }
+  __device__ __forceinline__ void key_copy(u64 slot, const uint8_t *src) const {
+    uint8_t *d = rec + slot * stride + 24;
+    copy_row(d, src, L);
+    for (u32 j = L; j < stride - 24; ++j) d[j] = 0;
+  }
+};
+
 // Tuning only (pdht_hip_set_phase_counters): shader-clock cycles per phase of
 // a scatter kernel, summed over workgroups.  Marks sit right after barriers,
 // so thread 0's clock stands for the workgroup's.  out == nullptr: off (one
@@ -338,11 +421,11 @@ constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL) {
 // identity ranking, 1 = no staging writes, 2 = no mbits/ptindex/index stores,
 // 3 = no key stores.
 // W waves x KPL groups per tile (default 4 x 16 = 4096 keys).
-template <int L, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false, int W = kStW, int KPL = kStKPL>
+template <int L, class Out, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false, int W = kStW,
+          int KPL = kStKPL>
 __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_scatter_staged(
-    const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
-    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
-    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out, u64 *__restrict__ prof) {
+    const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, u32 nbits, TileStarts ts, u64 ntiles,
+    Out out, u64 *__restrict__ prof) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                              // [kTile]
@@ -415,6 +498,31 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
     pc.mark(3);
     constexpr int kPer = kTile / kB;
     u32 gp[kPer];
+    if constexpr (Out::kPair8 && L == 8) {
+      // 8-B keys into 32-B records: two 16-B stores per record, {header,
+      // index} and {mbits, key}, half the store instructions of four 8-B ones
+      u64 hv[kPer];
+#pragma unroll
+      for (int jj = 0; jj < kPer; ++jj) {
+        const u32 j = min(jj * kB + threadIdx.x, tn - 1);
+        hv[jj] = stage[j];
+        gp[jj] = delta[(u32)rk.mod(hv[jj])] + j;
+        if (jj * kB + threadIdx.x < tn) out.head(gp[jj], tbase + sidx[j]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < KPL; ++g)
+        if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+      __syncthreads();
+#pragma unroll
+      for (int jj = 0; jj < kPer; ++jj) {
+        const u32 j = jj * kB + threadIdx.x;
+        if (j < tn) out.tail8(gp[jj], hv[jj], stage[j]);
+      }
+      __syncthreads();
+      pc.mark(5);
+      continue;
+    }
 #pragma unroll
     for (int jj = 0; jj < kPer; ++jj) {
       const u32 j = jj * kB + threadIdx.x;
@@ -422,12 +530,10 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
         const u64 hv = stage[j];
         gp[jj] = delta[(u32)rk.mod(hv)] + j;
         if (DBG & 4) continue;
-        mbits_out[gp[jj]] = hv;
-        if (ptindex_out) ptindex_out[gp[jj]] = (u32)pt.mod(hv);
-        if (index_out) index_out[gp[jj]] = tbase + sidx[j];
+        out.meta(gp[jj], hv, tbase + sidx[j]);
       }
     }
-    if (keys_out && !(DBG & 8)) {
+    if (out.has_keys() && !(DBG & 8)) {
 #pragma unroll
       for (int c = 0; c < L / 8; ++c) {
         __syncthreads();
@@ -439,7 +545,7 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
 #pragma unroll
         for (int jj = 0; jj < kPer; ++jj) {
           const u32 j = jj * kB + threadIdx.x;
-          if (j < tn) *reinterpret_cast<u64 *>(keys_out + (u64)gp[jj] * L + c * 8) = stage[j];
+          if (j < tn) out.key8(gp[jj], c, stage[j]);
         }
       }
     }
@@ -453,11 +559,10 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
 // Tile = W waves x KPL groups; keys, digests and ranks stay in VGPRs, so the
 // scatter pass issues no loads: on CDNA a load wait is a vmcnt wait, which
 // also counts the scattered stores already in flight.
-template <int W, int L, int KPL>
-__global__ __launch_bounds__(W * 64) void k_bucket_scatter_reg(
-    const uint8_t *__restrict__ keys, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
-    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
-    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out) {
+template <int W, int L, int KPL, class Out>
+__global__ __launch_bounds__(W * 64) void k_bucket_scatter_reg(const uint8_t *__restrict__ keys, u64 n,
+                                                               FastMod rk, u32 nranks, u32 nbits,
+                                                               TileStarts ts, u64 ntiles, Out out) {
   extern __shared__ u32 run[];  // [W][nranks]
   constexpr u64 kSub = (u64)KPL * 64, kTile = W * kSub;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -502,10 +607,8 @@ __global__ __launch_bounds__(W * 64) void k_bucket_scatter_reg(
       wave_lds_sync();
       if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
       if (valid) {
-        mbits_out[pos] = h[g];
-        if (ptindex_out) ptindex_out[pos] = (u32)pt.mod(h[g]);
-        if (index_out) index_out[pos] = i;
-        if (keys_out) store_key_row<L>(keys_out + (u64)pos * L, kr[g]);
+        out.meta(pos, h[g], i);
+        if (out.has_keys()) out.template key_row<L>(pos, kr[g]);
       }
       wave_lds_sync();
     }
@@ -514,26 +617,14 @@ __global__ __launch_bounds__(W * 64) void k_bucket_scatter_reg(
 }
 
 // ------------------------------------------------- generic-length scatter ---
-// Copy one L-byte key row (dword pieces when both rows are 4-B aligned).
-__device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L) {
-  if ((((uintptr_t)dst | (uintptr_t)src | L) & 3) == 0) {
-    const u32 *s = reinterpret_cast<const u32 *>(src);
-    u32 *d = reinterpret_cast<u32 *>(dst);
-    for (u32 j = 0; j < L / 4; ++j) d[j] = s[j];
-  } else {
-    for (u32 j = 0; j < L; ++j) dst[j] = src[j];
-  }
-}
-
 // Tile = W waves x 32 groups; wave w owns a contiguous 2048-key sub-range.
 // Counting pass hashes; the scatter pass hashes again from L2-resident keys
 // (32 unrolled generic-length hashes per lane do not fit in VGPRs).
 constexpr int kScatKPL = 32;
-template <int W>
-__global__ __launch_bounds__(W * 64) void k_bucket_scatter_wg(
-    const uint8_t *__restrict__ keys, u32 L, u64 n, FastMod pt, FastMod rk, u32 nranks, u32 nbits,
-    TileStarts ts, u64 ntiles, uint8_t *__restrict__ keys_out, u64 *__restrict__ mbits_out,
-    u32 *__restrict__ ptindex_out, u64 *__restrict__ index_out) {
+template <int W, class Out>
+__global__ __launch_bounds__(W * 64) void k_bucket_scatter_wg(const uint8_t *__restrict__ keys, u32 L, u64 n,
+                                                              FastMod rk, u32 nranks, u32 nbits,
+                                                              TileStarts ts, u64 ntiles, Out out) {
   extern __shared__ u32 run[];  // [W][nranks]
   constexpr u64 kSub = (u64)kScatKPL * 64, kTile = W * kSub;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -572,10 +663,8 @@ __global__ __launch_bounds__(W * 64) void k_bucket_scatter_wg(
       wave_lds_sync();
       if (valid && ahead == 0) myrun[r] += (u32)__builtin_popcountll(same);
       if (valid) {
-        mbits_out[pos] = h;
-        if (ptindex_out) ptindex_out[pos] = (u32)pt.mod(h);
-        if (index_out) index_out[pos] = i;
-        if (keys_out) copy_row(keys_out + (u64)pos * L, keys + i * (u64)L, L);
+        out.meta(pos, h, i);
+        if (out.has_keys()) out.key_copy(pos, keys + i * (u64)L);
       }
       wave_lds_sync();
     }

@@ -913,20 +913,16 @@ static int set_lds(const void *fn, size_t bytes) {
 struct BucketArgs {
   const uint8_t *k;
   u64 n;
-  FastMod pt, rk;
+  FastMod rk;
   u32 nranks, nbits;
   TileStarts ts;
   u64 ntiles;
-  uint8_t *ko;
-  u64 *mb;
-  u32 *pi;
-  u64 *ix;
 };
 
 // SERIAL: one group at a time in the tile-local ranking (variant 41, the r01
 // kernel) instead of the batched LDS atomics (rank_groups).
-template <int L, bool SERIAL = false, int DBG = 0, int W = kStW, int KPL = kStKPL>
-static int launch_staged(const BucketArgs &a, hipStream_t st, int dev) {
+template <int L, class Out, bool SERIAL = false, int DBG = 0, int W = kStW, int KPL = kStKPL>
+static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
   static const char *const serial_names[3] = {"k_bucket_scatter_staged<8B,serial-rank>",
@@ -937,57 +933,49 @@ static int launch_staged(const BucketArgs &a, hipStream_t st, int dev) {
   g_kernel = (W == 8 ? wide_names : SERIAL ? serial_names : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
   const size_t bytes = staged_lds_bytes(a.nranks, W, KPL);
   // the phase-clock build only while pdht_hip_set_phase_counters is active
-  auto fn = g_phase ? &k_bucket_scatter_staged<L, !SERIAL, DBG, true, W, KPL>
-                    : &k_bucket_scatter_staged<L, !SERIAL, DBG, false, W, KPL>;
+  auto fn = g_phase ? &k_bucket_scatter_staged<L, Out, !SERIAL, DBG, true, W, KPL>
+                    : &k_bucket_scatter_staged<L, Out, !SERIAL, DBG, false, W, KPL>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
   const int per_cu = env_int("PDHT_HIP_SCATTER_PER_CU", bytes <= 80 * 1024 ? 2 : 1);  // tuning only
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-  fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi,
-                               a.ix, g_phase);
+  fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, g_phase);
   return 0;
 }
 
-template <int W, int L, int KPL>
-static int launch_reg(const BucketArgs &a, hipStream_t st, int dev) {
+template <int W, int L, int KPL, class Out>
+static int launch_reg(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_reg<8B>", "k_bucket_scatter_reg<16B>",
                                        "k_bucket_scatter_reg<32B>"};
   g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
   const size_t bytes = (size_t)W * a.nranks * 4;
-  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_reg<W, L, KPL>), bytes)) return rc;
-  k_bucket_scatter_reg<W, L, KPL><<<grid_for(a.ntiles, 2, dev), W * 64, bytes, st>>>(
-      a.k, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi, a.ix);
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_reg<W, L, KPL, Out>), bytes)) return rc;
+  k_bucket_scatter_reg<W, L, KPL, Out><<<grid_for(a.ntiles, 2, dev), W * 64, bytes, st>>>(
+      a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
   return 0;
 }
 
-template <int W>
-static int launch_wg(const BucketArgs &a, u32 L, hipStream_t st, int dev) {
+template <int W, class Out>
+static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st, int dev) {
   g_kernel = W == 8 ? "k_bucket_scatter_wg<8>" : "k_bucket_scatter_wg<4>";
   const size_t bytes = (size_t)W * a.nranks * 4;
-  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_wg<W>), bytes)) return rc;
-  k_bucket_scatter_wg<W><<<grid_for(a.ntiles, 4, dev), W * 64, bytes, st>>>(
-      a.k, L, a.n, a.pt, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, a.ko, a.mb, a.pi, a.ix);
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_wg<W, Out>), bytes)) return rc;
+  k_bucket_scatter_wg<W, Out><<<grid_for(a.ntiles, 4, dev), W * 64, bytes, st>>>(
+      a.k, L, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
   return 0;
 }
 
 enum class BucketKernel { kStaged, kStagedWide, kReg, kGeneric };
-}  // namespace pdht
 
-PDHT_API int pdht_hip_set_phase_counters(uint64_t *buf) {
-  g_phase = buf;
-  return 0;
-}
-
-PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
-  return bucket_layout(nullptr, n, nranks).bytes;
-}
-
-PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
-                                   uint32_t nranks, void *workspace, size_t workspace_bytes,
-                                   void *keys_out, uint64_t *mbits_out, uint32_t *ptindex_out,
-                                   uint64_t *index_out, uint64_t *bucket_offsets,
-                                   pdht_hip_stream_t s) {
-  if (int rc = check_place(n, mbits_out, nptes, nranks, nullptr, 0)) return rc;
+// Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
+// (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
+// out_al: alignment bits of the output key rows (0 when they are 8-B aligned
+// 8-B pieces, as in records).
+template <class Out>
+static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nranks, void *workspace,
+                       size_t workspace_bytes, const Out &out, uintptr_t out_al, uint64_t *bucket_offsets,
+                       hipStream_t st) {
+  if (nranks == 0) return fail("nranks must be > 0%s", "");
   if (nranks > kBucketMaxRanks) return fail("bucketing supports up to 8192 ranks%s", "");
   if (n >= (1ull << 32)) return fail("bucketing: n must be < 2^32 per call%s", "");
   if (!bucket_offsets) return fail("bucket_offsets must not be NULL%s", "");
@@ -996,13 +984,12 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
   if (!workspace || workspace_bytes < w.bytes) return fail("workspace too small%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
-  hipStream_t st = ST(s);
   // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter up to
   // 2048 ranks, register scatter above; other lengths -> generic.  Variants:
   // 21 forces generic, 22 register, 41 staged with group-serial ranking (r01),
   // 43 staged with 8 waves x 8192-key tiles, 50-55 timing-only staged builds.
   const int variant = g_variant.load(std::memory_order_relaxed);
-  const uintptr_t al = (uintptr_t)keys | (uintptr_t)keys_out;
+  const uintptr_t al = (uintptr_t)keys | out_al;
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
   BucketKernel kind = !fixed || variant == 21                   ? BucketKernel::kGeneric
                       : variant == 22 || nranks > kStagedMaxRanks ? BucketKernel::kReg
@@ -1010,25 +997,20 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
                                                                   : BucketKernel::kStaged;
   const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
   const int reg_kpl = keysize == 32 ? 8 : 16;
-  const u64 tile = kind == BucketKernel::kStaged    ? kStTile
+  const u64 tile = kind == BucketKernel::kStaged       ? kStTile
                    : kind == BucketKernel::kStagedWide ? (u64)8 * kStKPL * 64
-                   : kind == BucketKernel::kReg  ? (u64)waves * reg_kpl * 64
-                                                 : (u64)waves * kScatKPL * 64;
+                   : kind == BucketKernel::kReg        ? (u64)waves * reg_kpl * 64
+                                                       : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   BucketArgs a{};
   a.k = static_cast<const uint8_t *>(keys);
   a.n = n;
-  a.pt = make_fastmod(nptes);
   a.rk = make_fastmod(nranks);
   a.nranks = nranks;
   while ((1u << a.nbits) < nranks) ++a.nbits;
   a.ts = TileStarts{w.counts, w.chunks, w.base, nranks};
   a.ntiles = ntiles;
-  a.ko = static_cast<uint8_t *>(keys_out);
-  a.mb = mbits_out;
-  a.pi = ptindex_out;
-  a.ix = index_out;
   const size_t hist_lds = (size_t)nranks * 4;
   if (ntiles) {
     const unsigned gc = grid_for(ntiles, 8, dev);
@@ -1053,33 +1035,69 @@ PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, u
   if (ntiles) {
     int rc = 0;
     if (kind == BucketKernel::kStagedWide)
-      rc = keysize == 8    ? launch_staged<8, false, 0, 8, kStKPL>(a, st, dev)
-           : keysize == 16 ? launch_staged<16, false, 0, 8, kStKPL>(a, st, dev)
-                           : launch_staged<32, false, 0, 8, kStKPL>(a, st, dev);
+      rc = keysize == 8    ? launch_staged<8, Out, false, 0, 8, kStKPL>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out, false, 0, 8, kStKPL>(a, out, st, dev)
+                           : launch_staged<32, Out, false, 0, 8, kStKPL>(a, out, st, dev);
     else if (kind == BucketKernel::kStaged && variant == 41)
-      rc = keysize == 8    ? launch_staged<8, true>(a, st, dev)
-           : keysize == 16 ? launch_staged<16, true>(a, st, dev)
-                           : launch_staged<32, true>(a, st, dev);
+      rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
+                           : launch_staged<32, Out, true>(a, out, st, dev);
     else if (kind == BucketKernel::kStaged && keysize == 8 && variant >= 50 && variant <= 55)
       // timing-only builds (wrong results): the r01 kernel with parts removed
-      rc = variant == 50   ? launch_staged<8, true, 1>(a, st, dev)
-           : variant == 51 ? launch_staged<8, true, 2>(a, st, dev)
-           : variant == 52 ? launch_staged<8, true, 4>(a, st, dev)
-           : variant == 53 ? launch_staged<8, true, 8>(a, st, dev)
-           : variant == 54 ? launch_staged<8, true, 12>(a, st, dev)
-                           : launch_staged<8, true, 15>(a, st, dev);
+      rc = variant == 50   ? launch_staged<8, Out, true, 1>(a, out, st, dev)
+           : variant == 51 ? launch_staged<8, Out, true, 2>(a, out, st, dev)
+           : variant == 52 ? launch_staged<8, Out, true, 4>(a, out, st, dev)
+           : variant == 53 ? launch_staged<8, Out, true, 8>(a, out, st, dev)
+           : variant == 54 ? launch_staged<8, Out, true, 12>(a, out, st, dev)
+                           : launch_staged<8, Out, true, 15>(a, out, st, dev);
     else if (kind == BucketKernel::kStaged)
-      rc = keysize == 8    ? launch_staged<8>(a, st, dev)
-           : keysize == 16 ? launch_staged<16>(a, st, dev)
-                           : launch_staged<32>(a, st, dev);
+      rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
+                           : launch_staged<32, Out>(a, out, st, dev);
     else if (kind == BucketKernel::kReg)
-      rc = keysize == 8    ? (waves == 8 ? launch_reg<8, 8, 16>(a, st, dev) : launch_reg<4, 8, 16>(a, st, dev))
-           : keysize == 16 ? (waves == 8 ? launch_reg<8, 16, 16>(a, st, dev) : launch_reg<4, 16, 16>(a, st, dev))
-                           : (waves == 8 ? launch_reg<8, 32, 8>(a, st, dev) : launch_reg<4, 32, 8>(a, st, dev));
+      rc = keysize == 8 ? (waves == 8 ? launch_reg<8, 8, 16>(a, out, st, dev) : launch_reg<4, 8, 16>(a, out, st, dev))
+           : keysize == 16
+               ? (waves == 8 ? launch_reg<8, 16, 16>(a, out, st, dev) : launch_reg<4, 16, 16>(a, out, st, dev))
+               : (waves == 8 ? launch_reg<8, 32, 8>(a, out, st, dev) : launch_reg<4, 32, 8>(a, out, st, dev));
     else
-      rc = waves == 8 ? launch_wg<8>(a, (u32)keysize, st, dev) : launch_wg<4>(a, (u32)keysize, st, dev);
+      rc = waves == 8 ? launch_wg<8>(a, out, (u32)keysize, st, dev) : launch_wg<4>(a, out, (u32)keysize, st, dev);
     if (rc) return rc;
   }
   HIP_TRY(hipGetLastError());
   return 0;
+}
+}  // namespace pdht
+
+PDHT_API int pdht_hip_set_phase_counters(uint64_t *buf) {
+  g_phase = buf;
+  return 0;
+}
+
+PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
+  return bucket_layout(nullptr, n, nranks).bytes;
+}
+
+PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
+                                   uint32_t nranks, void *workspace, size_t workspace_bytes,
+                                   void *keys_out, uint64_t *mbits_out, uint32_t *ptindex_out,
+                                   uint64_t *index_out, uint64_t *bucket_offsets,
+                                   pdht_hip_stream_t s) {
+  if (int rc = check_place(n, mbits_out, nptes, nranks, nullptr, 0)) return rc;
+  const OutSoA out{static_cast<uint8_t *>(keys_out), mbits_out, ptindex_out, index_out, make_fastmod(nptes),
+                   (u32)keysize};
+  return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, out, (uintptr_t)keys_out,
+                     bucket_offsets, ST(s));
+}
+
+PDHT_API size_t pdht_bucket_record_bytes(size_t keysize) { return 24 + ((keysize + 7) & ~(size_t)7); }
+
+PDHT_API int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n, uint32_t nranks,
+                                     uint32_t msg_type, uint32_t src_rank, uint32_t ht_index,
+                                     void *workspace, size_t workspace_bytes, void *records,
+                                     uint64_t *bucket_offsets, pdht_hip_stream_t s) {
+  if (n && !records) return fail("records must not be NULL%s", "");
+  if ((uintptr_t)records & 7) return fail("records must be 8-byte aligned%s", "");
+  const OutRec out{static_cast<uint8_t *>(records), (u64)pdht_bucket_record_bytes(keysize),
+                   (u64)msg_type | ((u64)src_rank << 32), ht_index, (u32)keysize};
+  return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, out, 0, bucket_offsets, ST(s));
 }

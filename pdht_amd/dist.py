@@ -123,6 +123,28 @@ def exchange_buckets(keys_out, mbits_out, offsets, index_out=None):
     return keys, mbits, index, recv
 
 
+def exchange_records(records, offsets):
+    """Ship wire records (pdht_amd.bucket_records with nranks == world size)
+    to their owner ranks: ONE all-to-all(v) of the record bytes instead of one
+    per payload (exchange_buckets).  Returns (records [m, stride] uint8,
+    recv_counts [world]): every record this rank owns, grouped by source rank
+    in rank order, each group in its source's key order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    if offsets.numel() != world + 1:
+        raise ValueError("bucket_records must have been called with nranks == world size")
+    rb = records.shape[1]
+    send = (offsets[1:] - offsets[:-1]).to(torch.int64)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    s_split = [int(x) * rb for x in send.cpu().tolist()]
+    r_split = [int(x) * rb for x in recv.cpu().tolist()]
+    out = torch.empty(sum(r_split), dtype=torch.uint8, device=records.device)
+    dist.all_to_all_single(out, records.contiguous().view(-1), r_split, s_split)
+    return out.view(-1, rb), recv
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:

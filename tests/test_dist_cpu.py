@@ -59,8 +59,18 @@ def _worker(rank, world, port, q):
         k2, m2, i2, cnt = D.exchange_buckets(torch.from_numpy(keys[order, :8].copy()),
                                              torch.from_numpy(mb[order].view(np.int64)),
                                              torch.from_numpy(offs.astype(np.int64)), gidx)
+        # the same bucket as wire records (the layout pdht_bucket_records_dev
+        # writes on a GPU, built here with numpy) shipped in ONE all-to-all(v)
+        rec = np.zeros((sh.n, P.bucket_record_bytes(8)), np.uint8)
+        rec[:, 0:4] = np.frombuffer(np.uint32(P.PDHT_PUT).tobytes(), np.uint8)
+        rec[:, 4:8] = np.frombuffer(np.uint32(r).tobytes(), np.uint8)
+        rec[:, 12:16] = order.astype(np.uint32).view(np.uint8).reshape(-1, 4)
+        rec[:, 16:24] = mb[order].view(np.uint8).reshape(-1, 8)
+        rec[:, 24:32] = keys[order, :8]
+        xr, xrc = D.exchange_records(torch.from_numpy(rec), torch.from_numpy(offs.astype(np.int64)))
         D.barrier()
         q.put({"rank": r, "first": sh.first, "n": sh.n, "local": local, "total": total,
+               "xrec": xr.numpy(), "xrcnt": xrc.numpy(),
                "max": mx, "ok_all": ok_all,
                "oracle_local": O.fold64(O.city64_fixed(keys), sh.first),
                "xkeys": k2.numpy(), "xmbits": m2.numpy().view(np.uint64), "xidx": i2.numpy(),
@@ -113,3 +123,12 @@ def test_two_rank_gloo_shards_and_reductions(oracle):
         assert (r["xkeys"] == whole[want, :8]).all()
         assert list(r["xcnt"]) == [int(((rk == r["rank"]) & (np.arange(len(rk)) // N_PER == s)).sum())
                                    for s in range(WORLD)]
+        # records: the same keys in the same order, header fields intact
+        xr = r["xrec"]
+        src = xr[:, 4:8].copy().view(np.uint32).ravel()
+        loc = xr[:, 12:16].copy().view(np.uint32).ravel()
+        assert (xr[:, 0:4].copy().view(np.uint32).ravel() == 1).all()
+        assert ((src.astype(np.int64) * N_PER + loc) == want).all()
+        assert (xr[:, 16:24].copy().view(np.uint64).ravel() == mb[want]).all()
+        assert (xr[:, 24:32] == whole[want, :8]).all()
+        assert (r["xrcnt"] == r["xcnt"]).all()

@@ -458,6 +458,42 @@ def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     assert (offs.cpu().numpy() == want_offs).all()
 
 
+RECORD_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 7, 1000, 2049, 8192)
+                for n in (0, 1, 4095, 100003)]
+RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 41, 43) for L in (8, 16, 32) for nr in (7, 1000, 2048)
+                 for n in (4097, 300007)]
+
+
+@pytest.mark.parametrize("L,nranks,n,variant", RECORD_CASES)
+def test_bucket_records(dev, oracle, L, nranks, n, variant):
+    """Wire records (message_t header + key) at the bucketed positions."""
+    rng = np.random.default_rng(L * 11 + nranks + n)
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    old = P.set_variant(variant)
+    try:
+        rec, offs = P.bucket_records(to_dev(k, dev), nranks, src_rank=5, ht_index=3)
+    finally:
+        P.set_variant(old)
+    rb = P.bucket_record_bytes(L)
+    assert rb == 24 + (L + 7) // 8 * 8 and tuple(rec.shape) == (n, rb)
+    m2, _, r2 = oracle.pdht_hash_fixed(k, 3, nranks) if n else (np.zeros(0, np.uint64), None,
+                                                                 np.zeros(0, np.uint32))
+    order = np.argsort(r2, kind="stable")
+    want_offs = np.concatenate([[0], np.cumsum(np.bincount(r2, minlength=nranks))])
+    assert (offs.cpu().numpy() == want_offs).all()
+    if n == 0:
+        return
+    R = rec.cpu().numpy()
+    w32 = R[:, :16].copy().view(np.uint32)
+    assert (w32[:, 0] == P.PDHT_PUT).all() and (w32[:, 1] == 5).all() and (w32[:, 2] == 3).all()
+    assert (w32[:, 3] == order).all()
+    assert (R[:, 16:24].copy().view(np.uint64).ravel() == m2[order]).all()
+    assert (R[:, 24:24 + L] == k[order]).all()
+    assert (R[:, 24 + L:] == 0).all()
+    ty, sr, hi, ix, mb, ko = P.record_fields(rec, L)
+    assert (u64(mb) == m2[order]).all() and (ix.cpu().numpy().view(np.uint32) == order).all()
+
+
 def test_place_golden_u64_keys(dev, golden):
     keys = np.arange(256, dtype=np.uint64).view(np.uint8).reshape(256, 8)
     kd = to_dev(keys, dev)

@@ -9,6 +9,7 @@ KiB.
 
   python tools/pmc_traffic.py --cfg cfg2 --keys 16777216 --kernel k_fixed_xpose64 \
       --dir gpurun_out --out profiles/traffic_cfg2.json
+  (--kernel "a|b|c" sums several kernels of one step, e.g. the bucketing launches)
 """
 import argparse
 import csv
@@ -38,8 +39,14 @@ def main():
     a = ap.parse_args()
     fd = a.fetch_dir or os.path.join(a.dir, "pmc_FETCH_SIZE")
     wd = a.write_dir or os.path.join(a.dir, "pmc_WRITE_SIZE")
-    f_kib, nf = per_launch(os.path.join(fd, "run_counter_collection.csv"), a.kernel, "FETCH_SIZE")
-    w_kib, nw = per_launch(os.path.join(wd, "run_counter_collection.csv"), a.kernel, "WRITE_SIZE")
+    # --kernel "a|b|c": the step launches several kernels; sum their medians
+    f_kib = w_kib = 0.0
+    nf = nw = 0
+    for k in a.kernel.split("|"):
+        f, nf = per_launch(os.path.join(fd, "run_counter_collection.csv"), k, "FETCH_SIZE")
+        w, nw = per_launch(os.path.join(wd, "run_counter_collection.csv"), k, "WRITE_SIZE")
+        f_kib += f
+        w_kib += w
     fetch = f_kib * 1024 * 2  # gfx950: FETCH_SIZE = half of a wide streaming read
     write = w_kib * 1024
     algo = a.algo_bytes_per_key * a.keys
