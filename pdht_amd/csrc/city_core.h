@@ -247,6 +247,23 @@ PDHT_HD void round64(LongState &st, const Words<16> &c) {
   st.z = x;
 }
 
+// Tail-first initialisation from the last 64 bytes t (city.c:237-243),
+// except the "+ Fetch64(s)" of x, which the caller adds (the chunk-streaming
+// kernel only has the first chunk one step later).
+PDHT_HD void city64_long_init(const Words<16> &t, u64 len, LongState &st) {
+  const u64 x = t.w64(24);  // s+len-40
+  st.y = t.w64(48) + t.w64(8);
+  st.z = mix16(t.w64(16) + len, t.w64(40));
+  st.v = weak32_at(t, 0, len, st.z);
+  st.w = weak32_at(t, 32, st.y + kK1, x);
+  st.x = x * kK1;
+}
+
+// city.c:261-262
+PDHT_HD u64 city64_long_final(const LongState &st) {
+  return mix16(mix16(st.v.lo, st.w.lo) + smix(st.y) * kK1 + st.z, mix16(st.v.hi, st.w.hi) + st.x);
+}
+
 // city.c:224-263
 template <class R>
 PDHT_HD u64 city64(const R &s, u64 len) {
@@ -254,19 +271,11 @@ PDHT_HD u64 city64(const R &s, u64 len) {
   if (len <= 64) return len33to64(s, len);
   const u32 n = (u32)len;
   LongState st;
-  {  // tail-first initialisation from the last 64 bytes (city.c:237-243)
-    const Words<16> t = s.template span<64>(n - 64);
-    const u64 x = t.w64(24);  // s+len-40
-    st.y = t.w64(48) + t.w64(8);
-    st.z = mix16(t.w64(16) + len, t.w64(40));
-    st.v = weak32_at(t, 0, len, st.z);
-    st.w = weak32_at(t, 32, st.y + kK1, x);
-    st.x = x * kK1 + fetch64(s, 0);
-  }
+  city64_long_init(s.template span<64>(n - 64), len, st);
+  st.x += fetch64(s, 0);
   const u32 rounds = (u32)((len - 1) >> 6);
   for (u32 r = 0; r < rounds; ++r) round64(st, s.template span<64>(r << 6));
-  return mix16(mix16(st.v.lo, st.w.lo) + smix(st.y) * kK1 + st.z,
-               mix16(st.v.hi, st.w.hi) + st.x);
+  return city64_long_final(st);
 }
 
 // city.c:265-272

@@ -20,6 +20,8 @@
 // carry no inter-workgroup communication.
 #pragma once
 
+#include <type_traits>
+
 #include "city_core.h"
 
 namespace pdht {
@@ -557,6 +559,76 @@ __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restr
       }
       if (i < n) sink.put(i, algo(r, (u64)64));
     }
+  }
+  sink.flush();
+}
+
+// --------------------------------------------- chunk-streamed long keys ---
+// Fixed keys too long for a 64-key LDS window (keylen > 255 B; 16-B multiple
+// length and stride, 16-B aligned rows), CityHash64 and its seeded form.  The
+// >64-byte loop (city.c:236-260) consumes a key 64 bytes at a time, so a wave
+// streams the s-th 64-byte chunk of each of its 64 keys through a 4 KiB LDS
+// image per step: 4 LDS-DMA instructions of 16 keys x 64 B (the xpose64
+// swizzle applied on the source side, as in k_fixed_lds64), double-buffered
+// so chunk s+1 is in flight while chunk s is hashed, and each lane reads its
+// row back with 4 ds_read_b128.  Step 0 is the tail [L-64, L) (tail-first
+// initialisation), steps 1..R the chunks 0..R-1.  k_global (each lane walking
+// its own key with per-lane loads) is the fallback for other lengths.
+template <class A>
+struct IsCity64Algo {
+  static constexpr bool value = std::is_same<A, AlgoCity64>::value || std::is_same<A, AlgoCity64Seeds>::value;
+};
+
+template <class Algo, class Sink, int AUX = 0>
+__global__ __launch_bounds__(kBlock) void k_fixed_chunks(const uint8_t *__restrict__ keys, u64 stride, u32 L,
+                                                         u64 n, Algo algo, Sink sink) {
+  __shared__ __attribute__((aligned(16))) u32 tile[kWavesPerBlock][2][1024];  // 2 x 4 KiB per wave
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  const u32 rounds = (L - 1) >> 6;
+  // image slot g = 64j + lane holds quarter (g&3) ^ swz(k) of key k = g>>2
+  auto issue = [&](u64 t, u32 off, int b) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32 g = 64 * j + lane;
+      const u32 k = g >> 2, cq = g & 3;
+      const u64 key = min((t << 6) + k, n - 1);
+      const uint8_t *src = keys + key * stride + off + ((cq ^ ((k >> 2) & 3)) << 4);
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)src,
+                                       (void __attribute__((address_space(3))) *)&tile[wave][b][256 * j], 16, 0,
+                                       AUX);
+    }
+  };
+  for (u64 t = (u64)blockIdx.x * kWavesPerBlock + wave; t < ntiles; t += nwaves) {
+    const u64 i = (t << 6) + lane;
+    issue(t, L - 64, 0);  // the tail
+    issue(t, 0, 1);       // chunk 0
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    RegReader<16> r;
+    read_row_asm(lds_addr(&tile[wave][0][0]), lane, r);
+    LongState st;
+    city64_long_init(r.template span<64>(0), L, st);
+    for (u32 q = 0; q < rounds; ++q) {
+      const int cb = (q + 1) & 1;  // chunk q sits in buffer (q+1)&1
+      if (q + 1 < rounds) {
+        issue(t, (q + 1) << 6, cb ^ 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      read_row_asm(lds_addr(&tile[wave][cb][0]), lane, r);
+      const Words<16> c = r.template span<64>(0);
+      if (q == 0) st.x += c.w64(0);  // "x * k1 + Fetch64(s)" (city.c:243)
+      round64(st, c);
+    }
+    u64 h = city64_long_final(st);
+    if constexpr (std::is_same<Algo, AlgoCity64Seeds>::value) h = mix16(h - algo.s0, algo.s1);
+    if (i < n) sink.put(i, h);
   }
   sink.flush();
 }

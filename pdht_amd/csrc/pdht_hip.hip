@@ -246,6 +246,19 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
     } else if (variant == 27 || (variant != 28 && tile_bytes > 16384)) {
       // keys too long for a 64-key window (tools/longbench.py, r01)
       // the 16-B reader measured equal to dword loads (longbench r01): variant only
+      // k_fixed_chunks (variant 32): 0.36-0.47 of peak against k_global's
+      // 0.50-0.62 on 256 B - 8 KiB keys (longbench r01): one chunk of
+      // prefetch per wave keeps fewer bytes in flight than 32 waves of
+      // per-lane loads
+      if constexpr (IsCity64Algo<Algo>::value) {
+        if (al16 && stride % 16 == 0 && keylen % 16 == 0 && keylen > 64 && variant == 32) {
+          g_kernel = "k_fixed_chunks";
+          k_fixed_chunks<Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 4, dev), kBlock, 0, st>>>(
+              k, stride, (u32)keylen, n, algo, NtSink<Sink>::make(sink));
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+      }
       if (al16 && stride % 16 == 0 && variant == 30) {
         g_kernel = "k_global<fixed,a16>";
         k_global<false, Algo, SinkNt, true><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
