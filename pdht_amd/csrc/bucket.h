@@ -419,7 +419,8 @@ constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL) {
 }
 // DBG (timing-only builds, tools/bucketbench.py; results are wrong): bit 0 =
 // identity ranking, 1 = no staging writes, 2 = no mbits/ptindex/index stores,
-// 3 = no key stores.
+// 3 = no key stores, 4 = one ballot round instead of ceil(log2 nranks), 5 =
+// branch-free clamped stores (correct results; A/B of the store form).
 // W waves x KPL groups per tile (default 4 x 16 = 4096 keys).
 template <int L, class Out, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false, int W = kStW,
           int KPL = kStKPL>
@@ -459,8 +460,13 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
     __syncthreads();
     pc.mark(0);
 #pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
+    for (int g = 0; g < KPL; ++g) {
+      if constexpr (!(DBG & 32)) {
+        if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
+      } else {
+        atomicAdd(&myrun[rr[g]], q0 + g * 64 < tn ? 1u : 0u);  // no branch
+      }
+    }
     __syncthreads();
     pc.mark(1);
     u32 s = 0;
@@ -484,7 +490,7 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
 #pragma unroll
       for (int g = 0; g < KPL; ++g) lp[g] = q0 + g * 64;
     } else if constexpr (BATCHED_RANK) {
-      rank_groups<KPL>(myrun, rr, q0, tn, nbits, lp);
+      rank_groups<KPL>(myrun, rr, q0, tn, (DBG & 16) ? 1u : nbits, lp);
     } else {
       rank_groups_serial<KPL>(myrun, rr, q0, tn, nbits, lp);
     }
@@ -523,14 +529,32 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
       pc.mark(5);
       continue;
     }
+    // Entries past a partial tile's end repeat its last entry (the same bytes
+    // to the same slot): no per-entry branches, whose exec masks the
+    // compiler would otherwise keep in SGPRs (and spill) across the unrolled
+    // stores.
+    // Per-entry branches around the stores measured 12 % faster than clamped
+    // branch-free stores (DBG bit 5, variant 58), although the branch-free
+    // form has no SGPR spills (48 v_readlane instead of 712 in the phase):
+    // the compiler then batches each array's stores, and the store order
+    // changes how the runs meet in L2.
+    if constexpr (!(DBG & 32)) {
 #pragma unroll
-    for (int jj = 0; jj < kPer; ++jj) {
-      const u32 j = jj * kB + threadIdx.x;
-      if (j < tn) {
+      for (int jj = 0; jj < kPer; ++jj) {
+        const u32 j = jj * kB + threadIdx.x;
+        if (j < tn) {
+          const u64 hv = stage[j];
+          gp[jj] = delta[(u32)rk.mod(hv)] + j;
+          out.meta(gp[jj], hv, tbase + sidx[j]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < kPer; ++jj) {
+        const u32 j = min(jj * kB + threadIdx.x, tn - 1);
         const u64 hv = stage[j];
         gp[jj] = delta[(u32)rk.mod(hv)] + j;
-        if (DBG & 4) continue;
-        out.meta(gp[jj], hv, tbase + sidx[j]);
+        if (!(DBG & 4)) out.meta(gp[jj], hv, tbase + sidx[j]);
       }
     }
     if (out.has_keys() && !(DBG & 8)) {
@@ -544,8 +568,12 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
         __syncthreads();
 #pragma unroll
         for (int jj = 0; jj < kPer; ++jj) {
-          const u32 j = jj * kB + threadIdx.x;
-          if (j < tn) out.key8(gp[jj], c, stage[j]);
+          if constexpr (!(DBG & 32)) {
+            const u32 j = jj * kB + threadIdx.x;
+            if (j < tn) out.key8(gp[jj], c, stage[j]);
+          } else {
+            out.key8(gp[jj], c, stage[min(jj * kB + threadIdx.x, tn - 1)]);
+          }
         }
       }
     }

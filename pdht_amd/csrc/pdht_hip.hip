@@ -1063,6 +1063,13 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
            : variant == 53 ? launch_staged<8, Out, true, 8>(a, out, st, dev)
            : variant == 54 ? launch_staged<8, Out, true, 12>(a, out, st, dev)
                            : launch_staged<8, Out, true, 15>(a, out, st, dev);
+    else if (kind == BucketKernel::kStaged && keysize == 8 && variant == 58)
+      rc = launch_staged<8, Out, false, 32>(a, out, st, dev);  // A/B: branch-free stores (correct)
+    else if (kind == BucketKernel::kStaged && keysize == 8 && (variant == 56 || variant == 57))
+      // timing-only: the default kernel with one ballot round (56), and also
+      // without global stores (57)
+      rc = variant == 56 ? launch_staged<8, Out, false, 16>(a, out, st, dev)
+                         : launch_staged<8, Out, false, 28>(a, out, st, dev);
     else if (kind == BucketKernel::kStaged)
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
