@@ -296,7 +296,9 @@ __device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L
 // ------------------------------------------------------------- outputs ---
 // Where a bucketed key goes; slot = its position in the bucketed batch.
 // OutSoA (pdht_bucket_batch_dev): separate arrays, each but mbits optional.
-struct OutSoA {
+// NT: non-temporal stores (A/B, variant 59).
+template <bool NT = false>
+struct OutSoAT {
   static constexpr bool kPair8 = false;
   uint8_t *keys;
   u64 *mbits;
@@ -305,13 +307,13 @@ struct OutSoA {
   FastMod pt;
   u32 L;
   __device__ __forceinline__ void meta(u64 slot, u64 h, u64 i) const {
-    mbits[slot] = h;
-    if (ptindex) ptindex[slot] = (u32)pt.mod(h);
-    if (index) index[slot] = i;
+    st<NT>(h, mbits + slot);
+    if (ptindex) st<NT>((u32)pt.mod(h), ptindex + slot);
+    if (index) st<NT>(i, index + slot);
   }
   __device__ __forceinline__ bool has_keys() const { return keys != nullptr; }
   __device__ __forceinline__ void key8(u64 slot, int c, u64 v) const {  // key bytes [8c, 8c+8)
-    *reinterpret_cast<u64 *>(keys + slot * L + 8 * c) = v;
+    st<NT>(v, reinterpret_cast<u64 *>(keys + slot * L + 8 * c));
   }
   template <int LL>
   __device__ __forceinline__ void key_row(u64 slot, const RegReader<LL / 4> &k) const {
@@ -321,6 +323,7 @@ struct OutSoA {
     copy_row(keys + slot * L, src, L);
   }
 };
+typedef OutSoAT<false> OutSoA;
 
 // OutRec (pdht_bucket_records_dev): one wire record per key, laid out as the
 // MPI variant's request message (message_t, libmpipdht/pdht.h:120-127) with

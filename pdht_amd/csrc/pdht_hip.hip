@@ -1063,7 +1063,14 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
            : variant == 53 ? launch_staged<8, Out, true, 8>(a, out, st, dev)
            : variant == 54 ? launch_staged<8, Out, true, 12>(a, out, st, dev)
                            : launch_staged<8, Out, true, 15>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged && keysize == 8 && variant == 58)
+    else if (kind == BucketKernel::kStaged && keysize == 8 && variant == 59) {
+      if constexpr (std::is_same<Out, OutSoA>::value) {  // A/B: non-temporal stores
+        const OutSoAT<true> o2{out.keys, out.mbits, out.ptindex, out.index, out.pt, out.L};
+        rc = launch_staged<8, OutSoAT<true>>(a, o2, st, dev);
+      } else {
+        rc = launch_staged<8, Out>(a, out, st, dev);
+      }
+    } else if (kind == BucketKernel::kStaged && keysize == 8 && variant == 58)
       rc = launch_staged<8, Out, false, 32>(a, out, st, dev);  // A/B: branch-free stores (correct)
     else if (kind == BucketKernel::kStaged && keysize == 8 && (variant == 56 || variant == 57))
       // timing-only: the default kernel with one ballot round (56), and also

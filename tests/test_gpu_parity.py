@@ -452,7 +452,7 @@ BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1
                 for n in (0, 1, 4095, 100003)]
 BUCKET_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192)
                  for n in (4095, 300007)]
-BUCKET_CASES += [(8, nr, n, 58) for nr in (7, 1000, 2048) for n in (1, 4097, 300007)]
+BUCKET_CASES += [(8, nr, n, v) for v in (58, 59) for nr in (7, 1000, 2048) for n in (1, 4097, 300007)]
 BUCKET_CASES += [(L, nr, n, v) for v in (41, 43) for L in (8, 16, 32) for nr in (1, 7, 1000, 1025, 2048)
                  for n in (1, 2049, 300007)]
 
@@ -464,7 +464,7 @@ def _bucket_kernel(L, nranks, variant):
         return f"k_bucket_scatter_staged<{L}B,serial-rank>"
     if variant == 43 and L in (8, 16, 32) and nranks <= 2048:
         return f"k_bucket_scatter_staged<{L}B,8x16>"
-    if variant == 58 and L == 8 and nranks <= 2048:
+    if variant in (58, 59) and L == 8 and nranks <= 2048:
         return "k_bucket_scatter_staged<8B>"
     if variant != 21 and L in (8, 16, 32):
         kind = "reg" if variant == 22 or nranks > 2048 else "staged"
