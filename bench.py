@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (tools/kbench.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline")
     return ap.parse_args()
 
 

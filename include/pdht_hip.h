@@ -167,9 +167,13 @@ int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
                                pdht_hip_stream_t stream);
 
 /* ---- engine tuning / introspection -------------------------------------- */
-/* Kernel variant used by pdht_city64_batch_dev for 64-byte packed keys:
- * 0 = auto, 1 = direct (per-lane 16-B loads), 2 = LDS-transposed,
- * 3 = generic LDS window.  Returns the previous value. */
+/* Tuning / A-B only: selects an alternative kernel where one exists; 0 (the
+ * default) is the measured-best choice everywhere.  Numbers per path (see
+ * the launchers in pdht_amd/csrc/pdht_hip.hip and DESIGN.md §4): 64-B keys
+ * 1-9, 15, 26; generic lengths 3, 11, 14, 27, 28, 30, 32; variable-length
+ * 10, 12-14, 23, 24, 31; small keys and placement 16-20; bucketing 21, 22,
+ * 41, 43, 58, 59 (50-57 are timing-only builds with wrong results).
+ * Process-wide; returns the previous value. */
 int pdht_hip_set_variant(int variant);
 /* Name of the kernel the last batch call on this thread launched. */
 const char *pdht_hip_last_kernel(void);
