@@ -570,11 +570,17 @@ def citycrc128_batch_host(keys, out=None, device: int = 0):
     return out
 
 
-def place_batch_host(keys: np.ndarray, nptes: int, nranks: int, device: int = 0):
+def place_batch_host(keys: np.ndarray, nptes: int, nranks: int, device: int = 0, out=None):
+    """Host-resident fused placement; `out` = (mbits uint64[n], ptindex
+    uint32[n], rank uint32[n]) host arrays to fill (pinned ones, with pinned
+    keys, take the zero-copy path)."""
     n, L = _np_keys(keys)
-    mb = np.empty(n, dtype=np.uint64)
-    pt = np.empty(n, dtype=np.uint32)
-    rk = np.empty(n, dtype=np.uint32)
+    if out is not None:
+        mb, pt, rk = out
+    else:
+        mb = np.empty(n, dtype=np.uint64)
+        pt = np.empty(n, dtype=np.uint32)
+        rk = np.empty(n, dtype=np.uint32)
     _check(lib().pdht_place_batch_host(_host_ptr(keys), L, n, nptes, nranks, _host_ptr(mb),
                                        _host_ptr(pt), _host_ptr(rk), 4, device),
            "pdht_place_batch_host")

@@ -434,6 +434,36 @@ static bool is_pinned(const void *p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// Device-side address of pinned host memory (nullptr if p is not pinned or
+// not mapped for the device).
+static void *pinned_device_ptr(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  return a.devicePointer;
+}
+
+// Zero-copy host batch: run `launch()` (kernels on device addresses of pinned
+// host buffers) on `device` and wait for it.
+template <class Launch>
+static int zero_copy_run(int device, Launch launch) {
+  if (device < 0 || device >= kMaxDev) return fail("device index %s%lld out of range", "", device);
+  int prev = -1;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(device));
+  int rc = launch();
+  if (rc == 0) {
+    hipError_t e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) rc = fail("%s (zero-copy batch)", hipGetErrorString(e));
+  }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+static bool zero_copy_allowed() { return g_variant.load(std::memory_order_relaxed) != 61; }
+
 static int slot_reserve(Slot &s, size_t in_bytes, size_t out_bytes) {
   if (!s.st) HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
   if (!s.done) HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -531,6 +561,16 @@ static int host_fixed(const void *keys, size_t keylen, size_t n, size_t out_per_
   if (!keys || !out || keylen == 0) return fail("null pointer or zero keylen%s", "");
   const size_t per = std::max<size_t>(1, kChunkBytes / keylen);
   const bool pin_in = is_pinned(keys), pin_out = is_pinned(out);
+  // Pinned keys and digests: zero-copy.  The kernel itself reads the keys
+  // and writes the digests over PCIe, no staging copies: 0.87 vs 0.75
+  // Gkeys/s on 16M x 64 B (62 vs 54 GB/s of PCIe traffic, r01).  Variant 61
+  // keeps the chunked copy pipeline.
+  void *zk = pin_in && pin_out && zero_copy_allowed() ? pinned_device_ptr(keys) : nullptr;
+  void *zo = zk ? pinned_device_ptr(out) : nullptr;
+  if (zk && zo)
+    return zero_copy_run(device, [&] {
+      return launch(static_cast<const uint8_t *>(zk), n, static_cast<uint8_t *>(zo), nullptr);
+    });
   auto plan = [&](size_t c, size_t *a, size_t *b) {
     if (c * per >= n) return false;
     *a = c * per;
@@ -682,6 +722,19 @@ PDHT_API int pdht_place_batch_host(const void *keys, size_t keysize, size_t n, u
   const bool pin_m = is_pinned(mbits);
   const bool pin_p = ptindex && is_pinned(ptindex);
   const bool pin_r = rank && is_pinned(rank);
+  if (pin_in && pin_m && (!ptindex || pin_p) && (!rank || pin_r) && zero_copy_allowed()) {
+    // zero-copy: the placement kernel reads and writes the pinned buffers
+    void *zk = pinned_device_ptr(keys), *zm = pinned_device_ptr(mbits);
+    void *zp = ptindex ? pinned_device_ptr(ptindex) : nullptr;
+    void *zr = rank ? pinned_device_ptr(rank) : nullptr;
+    if (zk && zm && (!ptindex || zp) && (!rank || zr))
+      return zero_copy_run(device, [&] {
+        return launch_fixed(zk, keysize, keysize, n, AlgoCity64{},
+                            make_place_sink(static_cast<u64 *>(zm), static_cast<u32 *>(zp), zr, rank_stride,
+                                            nullptr, nptes, nranks),
+                            nullptr);
+      });
+  }
   // device output layout per chunk: [mbits u64 x per][ptindex u32 x per][rank u32 x per]
   const size_t o_pt = per * 8, o_rk = per * 12;
   auto plan = [&](size_t c, size_t *a, size_t *b) {
@@ -723,6 +776,15 @@ PDHT_API int pdht_city64_batch_var_host(const void *bytes, const uint64_t *offse
   if (n == 0) return 0;
   if (!bytes || !offsets || !out) return fail("null pointer%s", "");
   const bool pin_in = is_pinned(bytes), pin_out = is_pinned(out);
+  if (pin_in && pin_out && is_pinned(offsets) && zero_copy_allowed()) {
+    void *zb = pinned_device_ptr(bytes), *zf = pinned_device_ptr(offsets), *zo = pinned_device_ptr(out);
+    if (zb && zf && zo)
+      return zero_copy_run(device, [&] {
+        g_var_bytes_hint = offsets[n] - offsets[0];
+        return launch_var(zb, static_cast<const u64 *>(zf), 0, n, AlgoCity64{},
+                          Sink64{nullptr, static_cast<u64 *>(zo)}, nullptr);
+      });
+  }
   const size_t max_keys = kChunkBytes / 16;
   // chunk c covers keys [a, b) with at most kChunkBytes of key bytes (a key
   // longer than that gets a chunk of its own and a larger buffer)

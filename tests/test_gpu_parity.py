@@ -549,8 +549,22 @@ def test_host_resident_paths(dev, oracle):
     assert (P.city64_batch_host(k) == want).all()  # pageable: staged
     kp = torch.from_numpy(k).pin_memory()
     op = torch.empty(n, dtype=torch.int64).pin_memory()
-    P.city64_batch_host(kp, out=op)  # pinned: direct DMA
+    P.city64_batch_host(kp, out=op)  # pinned in and out: zero-copy kernel
     assert (op.numpy().view(np.uint64) == want).all()
+    op.zero_()
+    old = P.set_variant(61)  # pinned, through the chunked copy pipeline
+    try:
+        P.city64_batch_host(kp, out=op)
+    finally:
+        P.set_variant(old)
+    assert (op.numpy().view(np.uint64) == want).all()
+    # zero-copy on pointers inside pinned allocations (offset rows)
+    op2 = torch.zeros(n - 7, dtype=torch.int64).pin_memory()
+    P.city64_batch_host(kp[7:], out=op2)
+    assert (op2.numpy().view(np.uint64) == want[7:]).all()
+    o128 = torch.empty((1000, 2), dtype=torch.int64).pin_memory()
+    P.citycrc128_batch_host(kp[3:1003], out=o128)
+    assert (o128.numpy().view(np.uint64) == oracle.city128_fixed(k[3:1003], crc=True)).all()
     assert (P.citycrc128_batch_host(k[:300000]) == oracle.city128_fixed(k[:300000], crc=True)).all()
     data, offs = oracle.mixed_keys(600000)
     assert (P.city64_var_batch_host(data, offs) == oracle.city64_var(data, offs)).all()
@@ -558,6 +572,22 @@ def test_host_resident_paths(dev, oracle):
     mb, pt, rk = P.place_batch_host(k8, 3, 12)
     m2, p2, r2 = oracle.pdht_hash_fixed(k8, 3, 12)
     assert (mb == m2).all() and (pt == p2).all() and (rk == r2).all()
+
+    # every buffer pinned: the zero-copy paths (variable-length and placement)
+    def pinned(n_, dt):
+        return torch.zeros(n_ * np.dtype(dt).itemsize, dtype=torch.uint8).pin_memory().numpy().view(dt)
+    pdata = pinned(data.size, np.uint8)
+    pdata[:] = data
+    poffs = pinned(offs.size, np.uint64)
+    poffs[:] = offs
+    pout = pinned(offs.size - 1, np.uint64)
+    P.city64_var_batch_host(pdata, poffs, out=pout)
+    assert (pout == oracle.city64_var(data, offs)).all()
+    pk8 = pinned(k8.size, np.uint8).reshape(k8.shape)
+    pk8[:] = k8
+    outs = (pinned(len(k8), np.uint64), pinned(len(k8), np.uint32), pinned(len(k8), np.uint32))
+    P.place_batch_host(pk8, 3, 12, out=outs)
+    assert (outs[0] == m2).all() and (outs[1] == p2).all() and (outs[2] == r2).all()
 
 
 def test_pdht_hash_batch_default_and_plugin(dev, oracle):
