@@ -128,31 +128,32 @@ def test_long_keys_global_reader(dev, oracle, L):
 
 @pytest.mark.parametrize("L", [256, 272, 320, 1024, 8192])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 5000])
-def test_long_keys_chunk_stream(dev, oracle, L, n):
-    """k_fixed_chunks (variant 32: 64-B chunks of 64 keys streamed through
-    LDS): packed and strided rows, ragged tiles, seeded digests and fused
-    placement."""
-    old = P.set_variant(32)
+@pytest.mark.parametrize("variant,kernel", [(32, "k_fixed_chunks")])
+def test_long_keys_chunk_stream(dev, oracle, L, n, variant, kernel):
+    """The long-key CityHash64 variant k_fixed_chunks (32: 64-B chunks of 64
+    keys streamed through LDS): packed and strided rows, ragged tiles, seeded
+    digests and fused placement."""
+    old = P.set_variant(variant)
     try:
-        _chunk_stream_case(oracle, dev, L, n)
+        _chunk_stream_case(oracle, dev, L, n, kernel)
     finally:
         P.set_variant(old)
 
 
-def _chunk_stream_case(oracle, dev, L, n):
+def _chunk_stream_case(oracle, dev, L, n, kernel):
     rng = np.random.default_rng(L * 3 + n)
     for stride in (L, L + 48):
         flat = rng.integers(0, 256, (n, stride), dtype=np.uint8)
         k = flat[:, :L]
         kd = to_dev(flat, dev)[:, :L]
         got = u64(P.city64_batch(kd))
-        assert P.last_kernel() == "k_fixed_chunks"
+        assert P.last_kernel() == kernel
         want = oracle.city64_fixed(np.ascontiguousarray(k))
         assert (got == want).all(), (L, n, stride)
     kd = to_dev(np.ascontiguousarray(k), dev)
     s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
     got = u64(P.city64_seeds_batch(kd, s0, s1))
-    assert P.last_kernel() == "k_fixed_chunks"
+    assert P.last_kernel() == kernel
     assert [int(x) for x in got[:40]] == [oracle.city64_seeds(r.tobytes(), s0, s1) for r in k[:40]]
     mb, pt, rk = P.place_batch(kd, 7, 1000)
     m2, p2, r2 = oracle.pdht_hash_fixed(np.ascontiguousarray(k), 7, 1000)
