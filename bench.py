@@ -497,7 +497,7 @@ def check_records(P, torch, D, sh, keys, b, dev):
 
 def host_rate(P, torch, n, cfg):
     """Host-resident rate: pinned keys in, pinned digests out, through the
-    C-ABI's host entry point (zero-copy for pinned buffers; PCIe-bound)."""
+    C-ABI host entry point (zero-copy for pinned buffers; PCIe-bound)."""
     try:
         m = min(n, 16 * M)
         keys = torch.empty((m, 64), dtype=torch.uint8).pin_memory()
