@@ -649,3 +649,42 @@ def test_cfg5_shard0_of_1B(dev, folds):
     kd = device_keys(per, 64, dev=dev)
     d = P.city64_batch(kd)
     assert f"{gpu_fold(d, 0):016x}" == f["shards"][0]
+
+
+def test_batches_capture_in_hip_graph(dev, oracle):
+    """The batch entry points are capture-safe (no allocation, no
+    synchronisation): record hash, placement and bucketing in one hipGraph
+    (torch.cuda.CUDAGraph on ROCm), replay it on new keys, check bit-exact."""
+    n = 50_000
+    keys = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    k8 = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    pl = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+          torch.empty(n, dtype=torch.int32, device=dev))
+    ws = torch.empty(P.bucket_workspace_bytes(n, 1000), dtype=torch.uint8, device=dev)
+    bk = P.bucket_batch(k8, 3, 1000, workspace=ws)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up outside capture (lazy device init)
+        P.city64_batch(keys, out=out)
+        P.place_batch(k8, 3, 1000, out=pl)
+        P.bucket_batch(k8, 3, 1000, out=bk, workspace=ws)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        P.city64_batch(keys, out=out)
+        P.place_batch(k8, 3, 1000, out=pl)
+        P.bucket_batch(k8, 3, 1000, out=bk, workspace=ws)
+    for seed in (1, 2):
+        rng = np.random.default_rng(seed)
+        kh = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+        k8h = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+        keys.copy_(torch.from_numpy(kh))
+        k8.copy_(torch.from_numpy(k8h))
+        g.replay()
+        torch.cuda.synchronize()
+        assert (u64(out) == oracle.city64_fixed(kh)).all()
+        m2, p2, r2 = oracle.pdht_hash_fixed(k8h, 3, 1000)
+        assert (u64(pl[0]) == m2).all() and (pl[2].cpu().numpy().view(np.uint32) == r2).all()
+        order = np.argsort(r2, kind="stable")
+        assert (bk[3].cpu().numpy() == order).all() and (u64(bk[1]) == m2[order]).all()
