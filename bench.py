@@ -2,7 +2,7 @@
 """Benchmark: device-resident batch CityHash64 on 64-byte keys (BASELINE.json).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-                  [--config cfg2|cfg3|cfg4|cfg5|place|bucket|exchange|records|xrecords|long]
+                  [--config cfg1|cfg2|cfg3|cfg4|cfg5|place|bucket|exchange|records|xrecords|long]
 
 One step = one pass of the hot path (one kernel launch) over this GPU's batch
 of synthetic keys already resident in HBM.  Default workload = BASELINE
@@ -24,9 +24,17 @@ Rank 0 prints one JSON line.  Besides the contract fields it carries
                    XOR fold (calibrated_key_stream_GBps);
   cpu_baseline  -- the reference city.c (oracle/_ref, or the oracle port when
                    _ref is absent) timed on this host's cores over a bounded
-                   sample of the same keys (rank 0, N = 1 only);
+                   sample of the same keys, as BASELINE.md §3 specifies: cfg1
+                   one thread through per-key pdht_hash semantics (digest + both
+                   reductions of hash.c:27/:29), every other config all the
+                   cores this job may use (affinity capped by the cgroup CPU
+                   quota), CLOCK_MONOTONIC_RAW, best of 5 (rank 0, N = 1 only);
   host_resident -- the same hash with keys/digests in pinned host memory
-                   (H2D + kernel + D2H pipeline), N = 1 only;
+                   (zero-copy over PCIe); at N > 1 every rank measures its own
+                   GPU at the same time (one PCIe link each) -> per-rank rates
+                   and the aggregate;
+  per_rank      -- (N > 1) each rank's device, kernel time, Gkeys/s and
+                   roofline fraction, plus the RCCL world;
   parity        -- this run's digests of the whole shard checked against the
                    reference golden folds (tests/golden/config_folds.json);
                    no oracle code runs outside the cpu_baseline leg.
@@ -57,13 +65,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange", "records",
+                    choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange", "records",
                              "xrecords", "long"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
-    ap.add_argument("--variant", type=int, default=0, help="kernel variant (tools/kbench.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=0.5,
+                    help="wall budget of one CPU-baseline pass (best of 5 passes)")
     return ap.parse_args()
 
 
@@ -94,8 +102,6 @@ def main():
         import __graft_entry__
         __graft_entry__.build()
     import pdht_amd as P
-    if a.variant:
-        P.set_variant(a.variant)
 
     cfg = a.config
     # ---------------------------------------------------------- workload ---
@@ -142,11 +148,27 @@ def main():
             ko, mb, pt, ix, offs_ = P.bucket_batch(keys, 3, nr, with_ptindex=cfg == "bucket")
             bucketed.update(ko=ko, mb=mb, pt=pt, ix=ix, offs=offs_)
             if cfg == "exchange" and world > 1:
-                bucketed["x"] = D.exchange_buckets(ko, mb, offs_, ix + sh.first)
+                bucketed["x"] = D.exchange_buckets(ko, mb, offs_, (ix.long() & 0xFFFFFFFF) + sh.first)
         out = None
-        bytes_per_key = L + L + 8 + 8 + (4 if cfg == "bucket" else 0)
+        bytes_per_key = L + L + 8 + 4 + (4 if cfg == "bucket" else 0)
         workload = (f"{cfg}: destination bucketing of {n >> 20}M x 8B keys per GPU by "
                     f"CityHash64 % {nr}" + (" + all-to-all(v) exchange" if cfg == "exchange" else ""))
+        total_bytes_in = n * L
+    elif cfg == "cfg1":
+        # BASELINE configs[0]: 1M x 64 B keys through hash.c (CityHash64 +
+        # ptindex + rank); on the GPU: the fused placement batch (nptes 1 =
+        # PDHT_DEFAULT_NUM_PTES, pdht_impl.h:41; 4 ranks as in README.txt:22)
+        L = 64
+        n = a.keys_per_gpu or M
+        sh = D.weak_shard(rank, world, n)
+        words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
+        keys = words.view(torch.uint8).view(n, L)
+        hist = torch.zeros(4, dtype=torch.int64, device=dev)
+        outs = P.place_batch(keys, 1, 4, hist=hist)
+        out = outs[0]
+        step = lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)  # noqa: E731
+        bytes_per_key = 64 + 8 + 4 + 4
+        workload = f"cfg1: pdht_hash placement (mbits+ptindex+rank+hist) of {n >> 20}M x 64B keys per GPU"
         total_bytes_in = n * L
     elif cfg in ("cfg2", "cfg4", "cfg5", "place"):
         L = 8 if cfg == "place" else 64
@@ -224,7 +246,7 @@ def main():
     D.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    elapsed, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=dev)
+    elapsed_max, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=dev)
 
     # -------------------------------------------- achievable read stream ---
     calib = None
@@ -275,13 +297,13 @@ def main():
         parity = check_buckets(P, torch, D, sh, keys, bucketed, dev)
     else:
         extra = None
-        if cfg == "place":  # one fresh call: the timed ones accumulated into hist
+        if cfg in ("place", "cfg1"):  # one fresh call: the timed ones accumulated into hist
             hist.zero_()
-            extra = (*P.place_batch(keys, 3, 1024, hist=hist), hist)
+            extra = (*P.place_batch(keys, *((1, 4) if cfg == "cfg1" else (3, 1024)), hist=hist), hist)
         parity = check_parity(P, torch, D, cfg, sh, out, extra, dev)
 
     # ------------------------------------------------------- report ------
-    value = n * world * a.steps / elapsed / 1e9
+    value = n * world * a.steps / elapsed_max / 1e9
     achieved = bytes_per_key * n / (kern_ms / 1e3) / 1e9
     res = {
         "metric": METRIC if cfg in ("cfg2", "cfg5") else f"{cfg}: Gkeys/s and achieved HBM GB/s",
@@ -290,7 +312,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -302,32 +324,63 @@ def main():
         "hbm_GBps": round(achieved * world, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
-                     "traffic": load_traffic(cfg, n), "kernel_ms": round(kern_ms, 4),
+                     "traffic": load_traffic(cfg, n, kernel_name), "kernel": kernel_name,
+                     "kernel_ms": round(kern_ms, 4),
                      "kernel_ms_max_rank": round(kern_ms_max, 4),
                      "read_only_GBps": round(total_bytes_in / (kern_ms / 1e3) / 1e9, 1),
                      "calibrated_read_stream_GBps": calib,
                      "calibrated_key_stream_GBps": calib_key},
         "parity": parity,
     }
-    if rank == 0 and world == 1 and cfg in ("cfg2", "cfg4") and not a.no_host:
-        res["host_resident"] = host_rate(P, torch, n, cfg)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and cfg == "cfg2":
-        res["cpu_baseline"] = cpu_baseline(a.cpu_seconds, out)
+    if world > 1:
+        res["per_rank"] = per_rank_report(torch, D, dev, rank, local, world, n, bytes_per_key, kern_ms,
+                                          elapsed, a.steps, P)
+    if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:
+        hr = host_rate(P, torch, n, cfg, D, dev)
+        if rank == 0:
+            res["host_resident"] = hr
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds, out, P, torch)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def load_traffic(cfg, n):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass, if any."""
+def per_rank_report(torch, D, dev, rank, local, world, n, bytes_per_key, kern_ms, elapsed, steps, P):
+    """Every rank's own numbers (gathered): device, kernel time, Gkeys/s and
+    roofline fraction per GPU, and the RCCL world (per-GPU and
+    aggregate at 1/2/4/8 GPUs)."""
+    import socket
+
+    import torch.distributed as dist
+    props = torch.cuda.get_device_properties(dev)
+    mine = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": dev.index,
+            "name": props.name, "pci": f"{getattr(props, 'pci_domain_id', 0):04x}:"
+                                       f"{getattr(props, 'pci_bus_id', 0):02x}:"
+                                       f"{getattr(props, 'pci_device_id', 0):02x}",
+            "kernel_ms": round(kern_ms, 4),
+            "Gkeys_s": round(n / (kern_ms / 1e3) / 1e9, 3),
+            "frac": round(bytes_per_key * n / (kern_ms / 1e3) / 1e9 / PEAK_HBM_GBPS, 4),
+            "wall_Gkeys_s": round(n * steps / elapsed / 1e9, 3)}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return {"world_size": world, "backend": dist.get_backend(),
+            "ranks": allr,
+            "Gkeys_s": [r["Gkeys_s"] for r in allr], "frac": [r["frac"] for r in allr],
+            "aggregate_kernel_Gkeys_s": round(sum(r["Gkeys_s"] for r in allr), 3)}
+
+
+def load_traffic(cfg, n, kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes, only if
+    they were taken of exactly the kernel (and launch shape) that ran here."""
     p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             t = json.load(f)
-        if int(t.get("keys_per_launch", -1)) != n:
+        if int(t.get("keys_per_launch", -1)) != n or t.get("kernel_tag") != kernel:
             return None
         return t.get("hbm_bytes_per_launch")
     except Exception:
@@ -371,7 +424,21 @@ def check_parity(P, torch, D, cfg, sh, out, extra, dev):
     if folds is None:
         return "unchecked (tests/golden/config_folds.json missing)"
     msgs, ok = [], True
-    if cfg == "place":
+    if cfg == "cfg1":
+        f = folds.get("cfg1_pdht_hash_1M_x64", {})
+        pl = [x for x in f.get("placements", []) if x["nptes"] == 1 and x["nranks"] == 4]
+        if sh.first == 0 and sh.n == f.get("n") and pl:
+            mb, pt, rk, hist = extra
+            got = {"mbits": D.fold_tensor(mb, 0), "ptindex": D.fold_tensor(pt.to(torch.int64) & 0xFFFFFFFF, 0),
+                   "rank": D.fold_tensor(rk.to(torch.int64) & 0xFFFFFFFF, 0), "hist": D.fold_tensor(hist, 0)}
+            want = {"mbits": f["mbits"], "ptindex": pl[0]["ptindex"], "rank": pl[0]["rank"], "hist": pl[0]["hist"]}
+            bad = [k for k, v in got.items() if v != int(want[k], 16)]
+            ok = not bad
+            msgs.append(f"mbits, ptindex, rank and histogram folds {'==' if ok else '!='} reference golden "
+                        f"(cfg1, nptes 1, nranks 4)" + (f" (mismatch: {bad})" if bad else ""))
+        else:
+            msgs.append("no golden fold for this shard")
+    elif cfg == "place":
         r = sh.first // (16 * M)
         g = folds.get("place_8B_16M", {}).get("shards", [])
         if sh.n == 16 * M and sh.first % (16 * M) == 0 and r < len(g):
@@ -419,6 +486,7 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
         ok = not bad
         msgs.append(f"bucketed mbits, index and offsets folds {'==' if ok else '!='} reference golden "
                     f"(bucket shard {r})" + (f" (mismatch: {bad})" if bad else ""))
+    ix = ix.long() & 0xFFFFFFFF
     srt = torch.sort(ix).values
     perm = bool((srt == torch.arange(n, device=dev)).all().item())
     same = bool((ko == keys[ix]).all().item()) and bool((P.city64_batch(ko) == mb).all().item())
@@ -495,50 +563,156 @@ def check_records(P, torch, D, sh, keys, b, dev):
     return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
 
 
-def host_rate(P, torch, n, cfg):
+def host_rate(P, torch, n, cfg, D, dev):
     """Host-resident rate: pinned keys in, pinned digests out, through the
-    C-ABI host entry point (zero-copy for pinned buffers; PCIe-bound)."""
+    C-ABI host entry point (zero-copy for pinned buffers; PCIe-bound).  At
+    N > 1 every rank runs at the same time on its own GPU (its own PCIe
+    link): per-rank rates and the aggregate over the slowest rank."""
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
     try:
-        m = min(n, 16 * M)
+        m = min(n, 16 * M if world == 1 else 4 * M)
         keys = torch.empty((m, 64), dtype=torch.uint8).pin_memory()
-        keys.view(-1).view(torch.int64).copy_(P.splitmix64_fill(SEED_KEYS, 0, m * 8).cpu())
+        keys.view(-1).view(torch.int64).copy_(P.splitmix64_fill(SEED_KEYS, rank * m * 8, m * 8, device=dev).cpu())
         w = 2 if cfg == "cfg4" else 1
         out = torch.empty((m, w) if w == 2 else (m,), dtype=torch.int64).pin_memory()
         fn = P.citycrc128_batch_host if cfg == "cfg4" else P.city64_batch_host
-        fn(keys, out=out)  # warm-up (allocates the pipeline buffers)
+        fn(keys, out=out, device=dev.index)  # warm-up
         reps = 3
+        D.barrier()
         t0 = time.perf_counter()
         for _ in range(reps):
-            fn(keys, out=out)
+            fn(keys, out=out, device=dev.index)
         dt = (time.perf_counter() - t0) / reps
-        return {"value": round(m / dt / 1e9, 4), "unit": "Gkeys/s", "keys": m,
-                "GBps_pcie": round(m * (64 + 8 * w) / dt / 1e9, 2),
-                "note": "pinned host keys and digests; the kernel reads/writes them over PCIe (zero-copy)"}
+        D.barrier()
+        mine = {"Gkeys_s": round(m / dt / 1e9, 4), "GBps_pcie": round(m * (64 + 8 * w) / dt / 1e9, 2)}
+        res = {"value": mine["Gkeys_s"], "unit": "Gkeys/s", "keys": m, "GBps_pcie": mine["GBps_pcie"],
+               "note": "pinned host keys and digests; the kernel reads/writes them over PCIe (zero-copy)"}
+        if world > 1:
+            dtmax = D.allreduce_max([dt], device=dev)[0]
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+            res.update(value=round(m * world / dtmax / 1e9, 4), keys=m * world,
+                       per_rank_Gkeys_s=[r["Gkeys_s"] for r in allr],
+                       per_rank_GBps_pcie=[r["GBps_pcie"] for r in allr],
+                       note=res["note"] + f"; {world} GPUs at once, one PCIe link each; value = all keys / "
+                                          "slowest rank")
+        return res
     except Exception as e:  # pragma: no cover
         return {"error": str(e)}
 
 
-def cpu_baseline(budget_s: float, gpu_digests=None):
-    """Reference city.c (oracle/_ref) on this host's cores over a bounded
-    sample: 4M x 64B keys of the same stream, repeated to fill ~budget_s.
-    The reference's digests of the sample are compared with this run's GPU
-    digests of the same keys (gpu_digests: the first 4M of rank 0's batch)."""
+def host_cpus():
+    """CPUs this job may use: the affinity set capped by the cgroup v2 CPU
+    quota (a GPU box grants a share of a large host), plus the NUMA layout."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:
+        pass
+    nodes = []
+    base = "/sys/devices/system/node"
+    if os.path.isdir(base):
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                try:
+                    nodes.append({"node": int(d[4:]), "cpus": open(f"{base}/{d}/cpulist").read().strip()})
+                except OSError:
+                    pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"threads": use, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "nproc_online": os.cpu_count(), "numa_nodes": nodes}
+
+
+def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
+    """The reference city.c (oracle/_ref) on this host over a bounded sample
+    of the same workload, as BASELINE.md §3 specifies:
+      cfg1   one thread, per-key pdht_hash semantics (CityHash64 + hash.c:27
+             and :29's two reductions) over all 1M x 64 B keys;
+      others all the CPUs this job may use (host_cpus), contiguous slices;
+      cfg4/long the -msse4.2 build's CityHashCrc128 (pdht.mk:21, city.c:402).
+    Timer CLOCK_MONOTONIC_RAW (pdht_inline.h:33-41), one warm-up pass, then
+    best of 5 timed passes, each repeating the sample to fill ~budget_s.  The
+    reference's digests of its sample are compared with this run's GPU
+    digests of the same keys."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    s = 4 * M
-    keys = O.fixed_keys(s, 64)
-    secs, out, kind = O.time_city64(keys, threads, 1)
+    cpus = host_cpus()
+    thr = 1 if cfg == "cfg1" else cpus["threads"]
+    mode, offsets, L = 0, None, 64
+    fname = "CityHash64"
+    nptes = nranks = 1
+    if cfg == "cfg1":
+        s_n, mode, nptes, nranks = M, 2, 1, 4
+        data = O.fixed_keys(s_n, 64)
+        what = "all 1M x 64B keys of cfg1, per-key pdht_hash semantics (nptes 1, nranks 4)"
+    elif cfg in ("cfg2", "cfg5"):
+        s_n = 4 * M
+        data = O.fixed_keys(s_n, 64)
+        what = "the first 4M x 64B keys of the stream"
+    elif cfg == "cfg4":
+        s_n, mode, fname = 4 * M, 1, "CityHashCrc128"
+        data = O.fixed_keys(s_n, 64)
+        what = "the first 4M x 64B keys, CityHashCrc128 (-msse4.2 build)"
+    elif cfg == "long":
+        s_n, mode, fname, L = M // 4, 1, "CityHashCrc128", 1024
+        data = O.fixed_keys(s_n, 1024)
+        what = "the first 256K x 1KiB keys, CityHashCrc128 (CityHashCrc256 rounds, -msse4.2 build)"
+    elif cfg == "cfg3":
+        s_n = 4 * M
+        data, offsets = O.mixed_keys(s_n)
+        L = 0
+        what = "the first 4M mixed 16..256B keys of the stream (offset-indexed)"
+    elif cfg in ("place", "bucket", "exchange", "records", "xrecords"):
+        s_n, mode, nptes, nranks, L = 4 * M, 2, 3, 1024, 8
+        data = O.fixed_keys(s_n, 8)
+        what = ("the first 4M x 8B keys, pdht_hash semantics (nptes 3, nranks 1024)"
+                + ("; hashing and placement only, no bucketing" if cfg != "place" else ""))
+    else:
+        return None
+    try:
+        fn, kind = O.cpu_fn(fname)
+    except RuntimeError as e:
+        return {"error": str(e)}
+
+    outs = None
+
+    def run(reps):
+        return O.time_batch(mode, fn, data, s_n, offsets=offsets, L=L, threads=thr, reps=reps,
+                            nptes=nptes, nranks=nranks, outs=outs)
+
+    _, dig, pt_, rk_ = run(1)  # pages in the sample and the outputs
+    outs = (dig, pt_, rk_)
+    # warm-up: at least 1 s of the same work first (cores idling before the
+    # run need about that long to reach their steady clock; measured here)
+    t_w, secs = 0.0, float("inf")
+    while t_w < 1.0:
+        dt = run(1)[0]
+        t_w += dt
+        secs = min(secs, dt)
     reps = max(1, int(budget_s / max(secs, 1e-6)))
-    secs, out, kind = O.time_city64(keys, threads, reps)
+    best = min(run(reps)[0] for _ in range(5))
     ok = None
-    if gpu_digests is not None:
-        ok = bool((out == gpu_digests[:s].cpu().numpy().view(np.uint64)).all())
-    one, _, _ = O.time_city64(keys[: M // 2], 1, 1)
-    return {"value": round(s * reps / secs / 1e9, 4), "unit": "Gkeys/s", "cores": threads,
-            "kind": kind, "sample": f"{reps} passes over 4M x 64B keys ({threads} pthreads, "
-                                    f"{secs:.2f} s wall, {secs * threads:.1f} CPU-s)",
-            "single_thread_Gkeys_s": round((M // 2) / one / 1e9, 4),
-            "gpu_digests_equal_reference": ok}
+    if gpu_out is not None:
+        g = gpu_out.reshape(-1)[: dig.size].cpu().numpy().view(np.uint64)
+        if cfg == "cfg3" or cfg in ("cfg1", "cfg2", "cfg4", "cfg5", "long", "place"):
+            ok = bool((dig[: g.size] == g).all()) if g.size == dig.size else None
+    res = {"value": round(s_n * reps / best / 1e9, 4), "unit": "Gkeys/s", "cores": thr, "kind": kind,
+           "sample": f"{what}; {reps} passes per timing, best of 5 ({best:.2f} s wall, "
+                     f"{best * thr:.1f} CPU-s)",
+           "timer": "CLOCK_MONOTONIC_RAW", "host": cpus, "gpu_digests_equal_reference": ok}
+    if cfg in ("cfg2", "cfg5"):
+        # BASELINE.md §3's other leg on the same box: one thread through
+        # per-key pdht_hash over cfg1's 1M x 64 B keys
+        k1 = O.fixed_keys(M, 64)
+        _, d1, p1, r1 = O.time_batch(2, fn, k1, M, L=64, threads=1, reps=20, nptes=1, nranks=4)
+        one = min(O.time_batch(2, fn, k1, M, L=64, threads=1, reps=1, nptes=1, nranks=4,
+                               outs=(d1, p1, r1))[0] for _ in range(5))
+        res["cfg1_single_thread_pdht_hash_Gkeys_s"] = round(M / one / 1e9, 4)
+    return res
 
 
 if __name__ == "__main__":

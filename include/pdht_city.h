@@ -54,6 +54,11 @@ uint128 CityHashCrc128WithSeed(const char *s, size_t len, uint128 seed);
 /* citycrc.h:46 */
 void CityHashCrc256(const char *s, size_t len, uint64 *result);
 
+/* Exported (non-static) by the reference city.c although city.h does not
+ * declare them (city.c:173, :190); kept for link-level parity. */
+uint128 WeakHashLen32WithSeeds6(uint64 w, uint64 x, uint64 y, uint64 z, uint64 a, uint64 b);
+uint128 WeakHashLen32WithSeeds(const char *s, uint64 a, uint64 b);
+
 #ifdef __cplusplus
 }
 #endif

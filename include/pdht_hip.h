@@ -57,9 +57,11 @@ int pdht_city64_batch_dev(const void *keys, size_t stride, size_t keylen,
 int pdht_city64_seeds_batch_dev(const void *keys, size_t stride, size_t keylen,
                                 size_t n, uint64_t seed0, uint64_t seed1,
                                 uint64_t *out, pdht_hip_stream_t stream);
-/* CityHash64 over variable-length keys. */
-int pdht_city64_batch_var_dev(const void *bytes, const uint64_t *offsets,
-                              size_t n, uint64_t *out,
+/* CityHash64 over variable-length keys.  nbytes = key bytes the batch spans
+ * (offsets[n] - offsets[0]; 0 if unknown): it sizes the kernel's LDS window
+ * for the mean key length and is never used to address memory. */
+int pdht_city64_batch_var_dev(const void *bytes, size_t nbytes,
+                              const uint64_t *offsets, size_t n, uint64_t *out,
                               pdht_hip_stream_t stream);
 /* CityHash128 (city.h:80): out[2i] = first, out[2i+1] = second. */
 int pdht_city128_batch_dev(const void *keys, size_t stride, size_t keylen,
@@ -68,8 +70,8 @@ int pdht_city128_batch_dev(const void *keys, size_t stride, size_t keylen,
 int pdht_city128_seed_batch_dev(const void *keys, size_t stride, size_t keylen,
                                 size_t n, uint64_t seed_lo, uint64_t seed_hi,
                                 uint64_t *out, pdht_hip_stream_t stream);
-int pdht_city128_batch_var_dev(const void *bytes, const uint64_t *offsets,
-                               size_t n, uint64_t *out,
+int pdht_city128_batch_var_dev(const void *bytes, size_t nbytes,
+                               const uint64_t *offsets, size_t n, uint64_t *out,
                                pdht_hip_stream_t stream);
 /* CityHashCrc128 (citycrc.h:39). */
 int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen,
@@ -80,9 +82,9 @@ int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride,
                                    size_t keylen, size_t n, uint64_t seed_lo,
                                    uint64_t seed_hi, uint64_t *out,
                                    pdht_hip_stream_t stream);
-int pdht_citycrc128_batch_var_dev(const void *bytes, const uint64_t *offsets,
-                                  size_t n, uint64_t *out,
-                                  pdht_hip_stream_t stream);
+int pdht_citycrc128_batch_var_dev(const void *bytes, size_t nbytes,
+                                  const uint64_t *offsets, size_t n,
+                                  uint64_t *out, pdht_hip_stream_t stream);
 
 /* Fused placement = pdht_hash (libpdht/hash.c:25-30) over a batch of packed
  * keysize-byte keys:
@@ -107,14 +109,17 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * outputs, keys in their original order; bucket_offsets has nranks+1
  * entries.  Outputs at bucketed positions: mbits_out (required),
  * keys_out (keysize bytes per key), ptindex_out (% nptes), index_out
- * (original key index) -- each optional (NULL).  nranks <= 8192,
- * n < 2^32.  `workspace` (device) must hold pdht_bucket_workspace_bytes. */
+ * (original key index, uint32: n < 2^32) -- each optional (NULL): a caller
+ * holding index_out can gather keys itself and pass keys_out = NULL; with
+ * nptes == 1 (pdht's default, pdht_impl.h:41) every ptindex is 0 and
+ * ptindex_out is best NULL.  nranks <= 8192, n < 2^32.  `workspace`
+ * (device) must hold pdht_bucket_workspace_bytes. */
 size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint32_t nptes, uint32_t nranks, void *workspace,
                           size_t workspace_bytes, void *keys_out,
                           uint64_t *mbits_out, uint32_t *ptindex_out,
-                          uint64_t *index_out, uint64_t *bucket_offsets,
+                          uint32_t *index_out, uint64_t *bucket_offsets,
                           pdht_hip_stream_t stream);
 
 /* The same bucketing, written as one wire record per key instead of separate
@@ -166,21 +171,10 @@ int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
                                uint32_t lo, uint32_t hi, uint64_t *lens,
                                pdht_hip_stream_t stream);
 
-/* ---- engine tuning / introspection -------------------------------------- */
-/* Tuning / A-B only: selects an alternative kernel where one exists; 0 (the
- * default) is the measured-best choice everywhere.  Numbers per path (see
- * the launchers in pdht_amd/csrc/pdht_hip.hip and DESIGN.md §4): 64-B keys
- * 1-9, 15, 26; generic lengths 3, 11, 14, 27, 28, 30, 32; variable-length
- * 10, 12-14, 23, 24, 31; small keys and placement 16-20; bucketing 21, 22,
- * 41, 43, 58, 59 (50-57 are timing-only builds with wrong results).
- * Process-wide; returns the previous value. */
-int pdht_hip_set_variant(int variant);
-/* Name of the kernel the last batch call on this thread launched. */
+/* ---- introspection and calibration -------------------------------------- */
+/* Tag of the kernel (and launch shape) the last batch call on this thread
+ * launched, e.g. "k_fixed_xpose64<nt,d2>@3" (3 workgroups per CU). */
 const char *pdht_hip_last_kernel(void);
-/* Optional: total key bytes (offsets[n] - offsets[0]) of the NEXT variable-
- * length batch call on this thread, which then sizes its LDS window for the
- * mean key length instead of assuming short keys.  Used by one call only. */
-int pdht_hip_set_var_bytes_hint(uint64_t total_bytes);
 /* HBM calibration: stream `bytes` (multiple of 16, 16-B aligned) through a
  * read-only kernel with 16-B coalesced loads (nt != 0: non-temporal) and
  * XOR-fold them into *out (one uint64, device).  Gives the achievable read
@@ -195,15 +189,8 @@ int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out, pdht_hip_
 /* The same for offset-indexed keys: the variable-length kernel's window DMA,
  * offsets reads, LDS reads of every key byte and digest stores, with the hash
  * replaced by an XOR fold (out[i] = fold of key i; see tests). */
-int pdht_hip_key_stream_var_dev(const void *bytes, const uint64_t *offsets, size_t n, uint64_t *out,
-                                pdht_hip_stream_t stream);
-/* Tuning only (tools/bucketbench.py): while buf != NULL (device memory, at
- * least 16 uint64, zeroed by the caller), the bucketing scatter kernels add
- * the shader-clock cycles their workgroups spend in each phase into buf[0..5]
- * and the number of tiles into buf[8].  NULL (the default) turns it off.
- * Returns 0. */
-int pdht_hip_set_phase_counters(uint64_t *buf);
-
+int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets, size_t n,
+                                uint64_t *out, pdht_hip_stream_t stream);
 #ifdef __cplusplus
 }
 #endif

@@ -565,3 +565,95 @@ void oracle_apply128(oracle_city128_fn fn, const uint8_t *bytes,
   apply_job p = {NULL, fn, bytes, offsets, stride, len, 0, 0, out};
   apply_run(p, n, threads);
 }
+
+/* ---- the product's pdht_hashfunc over a batch ----------------------------- */
+/* n calls of a pdht_hashfunc (libpdht/pdht.h:196) over packed keys, as n calls
+ * of dht->hashfn (putget.c:53) would make them: lets the tests run the
+ * PRODUCT's scalar pdht_hash over a whole config (cfg1) in C.  rank8 is a
+ * ptl_process_t array (8 bytes per entry, .rank = the low 32 bits). */
+typedef void (*oracle_hashfunc)(void *dht, void *key, uint64_t *mbits, uint32_t *ptindex,
+                                void *rank);
+void oracle_apply_hashfn(oracle_hashfunc fn, void *dht, const uint8_t *keys, size_t keysize,
+                         size_t n, uint64_t *mbits, uint32_t *ptindex, uint64_t *rank8) {
+  for (size_t i = 0; i < n; ++i)
+    fn(dht, (void *)(keys + i * keysize), mbits + i, ptindex + i, rank8 + i);
+}
+
+/* ---- CPU baseline harness (bench.py cpu_baseline) ------------------------- */
+/* `threads` pthreads over contiguous slices, `reps` passes.  mode 0: out[i] =
+ * f64(key_i); 1: {out[2i], out[2i+1]} = f128(key_i); 2: pdht_hash semantics
+ * (libpdht/hash.c:25-30): out[i] = mbits = f64(key_i), pt[i] = mbits % nptes,
+ * rk[i] = mbits % nranks (run-time divisors, real divides as in the
+ * reference).  Keys fixed (key i at bytes + i*stride, len bytes) or
+ * offset-indexed (offsets != NULL).  Returns wall seconds measured with
+ * CLOCK_MONOTONIC_RAW (the clock of pdht_inline.h:33-41). */
+typedef struct {
+  int mode;
+  oracle_city64_fn f64;
+  oracle_city128_fn f128;
+  const uint8_t *bytes;
+  const uint64_t *off;
+  size_t stride, len, lo, hi;
+  int reps;
+  uint64_t nptes, nranks;
+  uint64_t *out;
+  uint32_t *pt, *rk;
+} bjob;
+
+static void *bworker(void *arg) {
+  bjob *j = (bjob *)arg;
+  for (int r = 0; r < j->reps; ++r) {
+    for (size_t i = j->lo; i < j->hi; ++i) {
+      const uint8_t *p;
+      size_t n;
+      if (j->off) {
+        p = j->bytes + j->off[i];
+        n = (size_t)(j->off[i + 1] - j->off[i]);
+      } else {
+        p = j->bytes + i * j->stride;
+        n = j->len;
+      }
+      if (j->mode == 1) {
+        oracle_u128 v = j->f128((const char *)p, n);
+        j->out[2 * i] = v.first;
+        j->out[2 * i + 1] = v.second;
+      } else {
+        const uint64_t m = j->f64((const char *)p, n);
+        j->out[i] = m;
+        if (j->mode == 2) {
+          j->pt[i] = (uint32_t)(m % j->nptes);
+          j->rk[i] = (uint32_t)(m % j->nranks);
+        }
+      }
+    }
+  }
+  return NULL;
+}
+
+double oracle_time_batch(int mode, void *fn, const uint8_t *bytes, const uint64_t *offsets,
+                         size_t stride, size_t len, size_t n, int threads, int reps,
+                         uint64_t nptes, uint64_t nranks, uint64_t *out, uint32_t *pt,
+                         uint32_t *rk) {
+  if (threads < 1) threads = 1;
+  if (threads > 512) threads = 512;
+  pthread_t tid[512];
+  bjob jobs[512];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC_RAW, &t0);
+  for (int t = 0; t < threads; ++t) {
+    bjob j = {mode, NULL, NULL, bytes, offsets, stride, len, 0, 0, reps, nptes ? nptes : 1,
+              nranks ? nranks : 1, out, pt, rk};
+    if (mode == 1)
+      j.f128 = (oracle_city128_fn)fn;
+    else
+      j.f64 = (oracle_city64_fn)fn;
+    j.lo = n * (size_t)t / (size_t)threads;
+    j.hi = n * (size_t)(t + 1) / (size_t)threads;
+    jobs[t] = j;
+    if (t > 0) pthread_create(&tid[t], NULL, bworker, &jobs[t]);
+  }
+  bworker(&jobs[0]);
+  for (int t = 1; t < threads; ++t) pthread_join(tid[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC_RAW, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

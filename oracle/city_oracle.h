@@ -93,6 +93,18 @@ void oracle_apply128(oracle_city128_fn fn, const uint8_t *bytes,
                      const uint64_t *offsets, size_t stride, size_t len,
                      size_t n, uint64_t *out /* 2n */, int threads);
 
+/* The product's pdht_hashfunc driven over a batch (tests: cfg1). */
+typedef void (*oracle_hashfunc)(void *dht, void *key, uint64_t *mbits, uint32_t *ptindex,
+                                void *rank);
+void oracle_apply_hashfn(oracle_hashfunc fn, void *dht, const uint8_t *keys, size_t keysize,
+                         size_t n, uint64_t *mbits, uint32_t *ptindex, uint64_t *rank8);
+/* CPU baseline harness (bench.py): mode 0 = 64-bit digest, 1 = 128-bit,
+ * 2 = pdht_hash semantics (digest + both reductions). */
+double oracle_time_batch(int mode, void *fn, const uint8_t *bytes, const uint64_t *offsets,
+                         size_t stride, size_t len, size_t n, int threads, int reps,
+                         uint64_t nptes, uint64_t nranks, uint64_t *out, uint32_t *pt,
+                         uint32_t *rk);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,6 +84,13 @@ def lib():
         L.oracle_time_city64.restype = C.c_double
         L.oracle_time_city64.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
                                          C.c_int, C.c_int, C.c_void_p]
+        L.oracle_apply_hashfn.restype = None
+        L.oracle_apply_hashfn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_time_batch.restype = C.c_double
+        L.oracle_time_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                        C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_uint64,
+                                        C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         for name in ("oracle_apply64", "oracle_apply128"):
             f = getattr(L, name)
             f.restype = None
@@ -309,3 +316,52 @@ def apply_ref128(bytes_: np.ndarray, n: int, *, offsets=None, L: int = 0,
     offp = _buf(np.ascontiguousarray(offsets, dtype=np.uint64)) if offsets is not None else None
     lib().oracle_apply128(fn, _buf(bytes_), offp, L, L, n, _buf(out), threads)
     return out
+
+
+def apply_hashfn(fn_ptr: int, dht_ptr: int, keys: np.ndarray):
+    """n calls of a pdht_hashfunc (e.g. the PRODUCT's pdht_hash) over packed
+    keys [n, keysize], in C.  Returns (mbits u64[n], ptindex u32[n], rank
+    u32[n]); ptindex is pre-filled with 0xFFFFFFFF so an implementation that
+    leaves it untouched (libmpipdht/hash.c:6-9) is visible."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    n, L = keys.shape
+    m = np.empty(n, np.uint64)
+    p = np.full(n, 0xFFFFFFFF, np.uint32)
+    r = np.zeros(n, np.uint64)  # ptl_process_t[n]
+    lib().oracle_apply_hashfn(C.c_void_p(fn_ptr), C.c_void_p(dht_ptr), _buf(keys), L, n, _buf(m), _buf(p),
+                              _buf(r))
+    return m, p, (r & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def cpu_fn(name: str = "CityHash64", use_ref: bool = True):
+    """(function pointer, kind) of a CityHash function for the CPU baseline:
+    the reference city.c (oracle/_ref, kind "reference") when built, else the
+    oracle port (kind "port")."""
+    R = ref() if use_ref else None
+    if R is not None:
+        return C.cast(getattr(R, name), C.c_void_p).value, "reference"
+    port = {"CityHash64": "oracle_city64_c"}
+    if name not in port:
+        raise RuntimeError(f"no port of {name} for the CPU baseline (oracle/_ref not built)")
+    return C.cast(getattr(lib(), port[name]), C.c_void_p).value, "port"
+
+
+def time_batch(mode: int, fn: int, data: np.ndarray, n: int, *, offsets=None, L: int = 0,
+               threads: int = 1, reps: int = 1, nptes: int = 1, nranks: int = 1, outs=None):
+    """Wall seconds (CLOCK_MONOTONIC_RAW) of `reps` passes over a batch with
+    `threads` pthreads; mode 0 = 64-bit digests, 1 = 128-bit, 2 = pdht_hash
+    semantics (hash.c:25-30).  Returns (secs, digests, ptindex, rank).
+    `outs` = (digests, ptindex, rank) of an earlier call to reuse: fresh
+    arrays would put their first-touch page faults inside the timing."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if outs is not None:
+        out, pt, rk = outs
+    else:
+        out = np.zeros(2 * n if mode == 1 else n, np.uint64)
+        pt = np.zeros(n, np.uint32) if mode == 2 else None
+        rk = np.zeros(n, np.uint32) if mode == 2 else None
+    offp = _buf(np.ascontiguousarray(offsets, dtype=np.uint64)) if offsets is not None else None
+    secs = lib().oracle_time_batch(mode, C.c_void_p(fn), _buf(data), offp, L, L, n, threads, reps, nptes,
+                                   nranks, _buf(out), _buf(pt) if pt is not None else None,
+                                   _buf(rk) if rk is not None else None)
+    return secs, out, pt, rk

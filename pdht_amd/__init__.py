@@ -34,7 +34,8 @@ __all__ = [
     "citycrc128_var_batch", "place_batch", "city64_batch_host", "city64_var_batch_host",
     "citycrc128_batch_host", "place_batch_host", "splitmix64_fill", "mixed_lengths",
     "device_count", "PdhtTable", "K2", "bucket_batch", "bucket_records", "record_fields",
-    "bucket_record_bytes", "bucket_workspace_bytes",
+    "bucket_record_bytes", "bucket_workspace_bytes", "WeakHashLen32WithSeeds", "WeakHashLen32WithSeeds6",
+    "tuning", "last_kernel",
 ]
 
 K2 = 0x9AE16A3B2F90404F  # city.c:96 (CityHash64WithSeed's seed0)
@@ -69,32 +70,33 @@ class _PdhtT(C.Structure):
     _fields_ = [("keysize", C.c_uint), ("hashfn", C.c_void_p), ("nptes", C.c_uint)]
 
 
-_lib = None
+_lib = None        # the library the wrappers call (product, or tuning inside tuning())
+_product = None
+_tuning = None
 _V = C.c_void_p
 _S = C.c_size_t
 _U64 = C.c_uint64
 _U32 = C.c_uint32
+TUNING_LIB_PATH = os.path.join(HERE, "lib", "libpdht_hip_tuning.so")
+MPI_LIB_PATH = os.path.join(HERE, "lib", "libpdht_hip_mpi.so")
 
 
-def _declare(L):
+def _declare(L, tuning=False):
     sig = {
         "pdht_hip_version": (C.c_char_p, []),
         "pdht_hip_last_error": (C.c_char_p, []),
         "pdht_hip_last_kernel": (C.c_char_p, []),
-        "pdht_hip_set_var_bytes_hint": (C.c_int, [C.c_uint64]),
-        "pdht_hip_set_variant": (C.c_int, [C.c_int]),
-        "pdht_hip_set_phase_counters": (C.c_int, [_V]),
         "pdht_hip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
         "pdht_hip_set_device": (C.c_int, [C.c_int]),
         "pdht_city64_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
         "pdht_city64_seeds_batch_dev": (C.c_int, [_V, _S, _S, _S, _U64, _U64, _V, _V]),
-        "pdht_city64_batch_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_city64_batch_var_dev": (C.c_int, [_V, _S, _V, _S, _V, _V]),
         "pdht_city128_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
         "pdht_city128_seed_batch_dev": (C.c_int, [_V, _S, _S, _S, _U64, _U64, _V, _V]),
-        "pdht_city128_batch_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_city128_batch_var_dev": (C.c_int, [_V, _S, _V, _S, _V, _V]),
         "pdht_citycrc128_batch_dev": (C.c_int, [_V, _S, _S, _S, _V, _V]),
         "pdht_citycrc128_seed_batch_dev": (C.c_int, [_V, _S, _S, _S, _U64, _U64, _V, _V]),
-        "pdht_citycrc128_batch_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_citycrc128_batch_var_dev": (C.c_int, [_V, _S, _V, _S, _V, _V]),
         "pdht_place_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _V, _V, _S, _V, _V]),
         "pdht_city64_batch_host": (C.c_int, [_V, _S, _S, _V, C.c_int]),
         "pdht_city64_batch_var_host": (C.c_int, [_V, _V, _S, _V, C.c_int]),
@@ -104,7 +106,7 @@ def _declare(L):
         "pdht_hip_mixed_lengths_dev": (C.c_int, [_U64, _U64, _S, _U32, _U32, _V, _V]),
         "pdht_hip_read_stream_dev": (C.c_int, [_V, _S, C.c_int, _V, _V]),
         "pdht_hip_key_stream_dev": (C.c_int, [_V, _S, _V, _V]),
-        "pdht_hip_key_stream_var_dev": (C.c_int, [_V, _V, _S, _V, _V]),
+        "pdht_hip_key_stream_var_dev": (C.c_int, [_V, _S, _V, _S, _V, _V]),
         "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _U32]),
         "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
         "pdht_bucket_record_bytes": (C.c_size_t, [_S]),
@@ -117,6 +119,8 @@ def _declare(L):
         "CityHashCrc128": (Uint128, [_V, _S]),
         "CityHashCrc128WithSeed": (Uint128, [_V, _S, Uint128]),
         "CityHashCrc256": (None, [_V, _S, C.POINTER(C.c_uint64)]),
+        "WeakHashLen32WithSeeds": (Uint128, [_V, _U64, _U64]),
+        "WeakHashLen32WithSeeds6": (Uint128, [_U64, _U64, _U64, _U64, _U64, _U64]),
         "pdht_hash": (None, [_V, _V, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
                              C.POINTER(PtlProcess)]),
         "pdht_sethash": (None, [_V, _V]),
@@ -124,24 +128,62 @@ def _declare(L):
         "pdht_hash_batch_dev": (C.c_int, [_V, _V, _S, _V, _V, _V, _V, _V]),
         "pdht_hip_table_init": (None, [_V, C.c_uint, C.c_uint]),
     }
+    if tuning:
+        sig["pdht_hip_set_variant"] = (C.c_int, [C.c_int])
+        sig["pdht_hip_set_blocks_per_cu"] = (C.c_int, [C.c_int])
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
 
 
+def _load(path, tuning=False):
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `make -C {ROOT}` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    L = C.CDLL(path)
+    _declare(L, tuning)
+    return L
+
+
 def lib():
-    """The product library (loaded once).  Raises if it was not built."""
-    global _lib
+    """The library the batch wrappers call: the product libpdht_hip.so (loaded
+    once), or the tuning build inside a `tuning()` block.  Raises if it was
+    not built."""
+    global _lib, _product
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(
-                f"{LIB_PATH} is missing: build it with `make -C {ROOT}` or "
-                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
-        L = C.CDLL(LIB_PATH)
-        _declare(L)
-        _lib = L
+        _product = _load(LIB_PATH)
+        _lib = _product
     return _lib
+
+
+class tuning:
+    """Context manager for tools/ and the A/B tests: route every wrapper
+    through libpdht_hip_tuning.so (same sources, -DPDHT_HIP_TUNING) with
+    kernel variant `variant` and, optionally, `per_cu` workgroups per CU.
+    The product library has no variants and no tuning entry points."""
+
+    def __init__(self, variant: int = 0, per_cu: int = 0):
+        self.variant, self.per_cu = variant, per_cu
+
+    def __enter__(self):
+        global _lib, _tuning
+        lib()
+        if _tuning is None:
+            _tuning = _load(TUNING_LIB_PATH, tuning=True)
+        self._prev = _lib
+        self._old = (_tuning.pdht_hip_set_variant(self.variant),
+                     _tuning.pdht_hip_set_blocks_per_cu(self.per_cu))
+        _lib = _tuning
+        return self
+
+    def __exit__(self, *exc):
+        global _lib
+        _tuning.pdht_hip_set_variant(self._old[0])
+        _tuning.pdht_hip_set_blocks_per_cu(self._old[1])
+        _lib = self._prev
+        return False
 
 
 def _check(rc: int, what: str):
@@ -151,17 +193,6 @@ def _check(rc: int, what: str):
 
 def last_kernel() -> str:
     return lib().pdht_hip_last_kernel().decode()
-
-
-def set_variant(v: int) -> int:
-    return lib().pdht_hip_set_variant(v)
-
-
-def set_phase_counters(buf=None) -> None:
-    """Tuning only: per-phase clock totals of the bucketing scatter kernels are
-    added into buf (int64[>=16], CUDA, zeroed) while set; None turns it off."""
-    _check(lib().pdht_hip_set_phase_counters(_dptr(buf) if buf is not None else None),
-           "pdht_hip_set_phase_counters")
 
 
 def device_count() -> int:
@@ -224,26 +255,88 @@ def CityHashCrc256(data) -> tuple[int, int, int, int]:
     return tuple(out)
 
 
+def WeakHashLen32WithSeeds(data, a: int, b: int) -> tuple[int, int]:
+    """city.c:190-198 (reads 32 bytes of data)."""
+    p, n = _cbuf(data)
+    if n < 32:
+        raise ValueError("WeakHashLen32WithSeeds reads 32 bytes")
+    r = lib().WeakHashLen32WithSeeds(p, a, b)
+    return r.first, r.second
+
+
+def WeakHashLen32WithSeeds6(w: int, x: int, y: int, z: int, a: int, b: int) -> tuple[int, int]:
+    """city.c:173-187"""
+    r = lib().WeakHashLen32WithSeeds6(w, x, y, z, a, b)
+    return r.first, r.second
+
+
 # ----------------------------------------------------- device batch API ---
+# Every device wrapper launches on the device its tensors live on: the C-ABI
+# sizes grids for, and launches on, the CURRENT device, so each call runs
+# under `with torch.cuda.device(<tensor's device>)` on that device's stream
+# (the caller's `stream`, which must belong to the same device, or the
+# device's current stream).  Every tensor handed to C is checked for device,
+# dtype, contiguity and size first: a wrong one raises instead of letting a
+# kernel write past its end.
 def _torch():
     import torch
     return torch
 
 
-def _stream_ptr(stream=None):
-    torch = _torch()
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return C.c_void_p(s.cuda_stream)
+class _on:
+    """Device guard + stream of one device-side call."""
+
+    def __init__(self, device, stream=None):
+        torch = _torch()
+        if device.type != "cuda":
+            raise ValueError("expected CUDA tensors")
+        self.device = device
+        self.guard = torch.cuda.device(device)
+        self.stream_obj = stream
+        if stream is not None and stream.device != device:
+            raise ValueError(f"stream is on {stream.device}, tensors on {device}")
+
+    def __enter__(self):
+        torch = _torch()
+        self.guard.__enter__()
+        s = self.stream_obj if self.stream_obj is not None else torch.cuda.current_stream(self.device)
+        self.stream = C.c_void_p(s.cuda_stream)
+        return self
+
+    def __exit__(self, *exc):
+        return self.guard.__exit__(*exc)
 
 
 def _dptr(t) -> C.c_void_p:
     return C.c_void_p(t.data_ptr())
 
 
+def _opt(t):
+    return _dptr(t) if t is not None else None
+
+
+def _need(t, name, dtype, device, numel=None, shape=None):
+    """A CUDA tensor of `dtype` on `device`, contiguous, with >= numel
+    elements (or exactly `shape`)."""
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if not getattr(t, "is_cuda", False) or t.device != device:
+        raise ValueError(f"{name} must be a CUDA tensor on {device}")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"{name} must hold >= {numel} elements, got {t.numel()}")
+    return t
+
+
 def _keys_2d(keys):
     """keys: uint8 CUDA tensor [n, L] with unit inner stride (rows may be strided)."""
     torch = _torch()
-    if keys.dtype != torch.uint8 or keys.dim() != 2 or not keys.is_cuda:
+    if not isinstance(keys, torch.Tensor) or keys.dtype != torch.uint8 or keys.dim() != 2 or not keys.is_cuda:
         raise ValueError("keys must be a CUDA uint8 tensor of shape [n, keylen]")
     n, L = keys.shape
     if keys.stride(1) != 1 and L > 1 and n > 0:
@@ -257,25 +350,25 @@ def _out(n, words, device, out=None):
     shape = (n,) if words == 1 else (n, words)
     if out is None:
         return torch.empty(shape, dtype=torch.int64, device=device)
-    if out.dtype != torch.int64 or tuple(out.shape) != shape or not out.is_contiguous():
-        raise ValueError(f"out must be a contiguous int64 tensor of shape {shape}")
-    return out
+    return _need(out, "out", torch.int64, device, shape=shape)
 
 
 def city64_batch(keys, out=None, stream=None):
     """CityHash64 of each row of keys [n, L] (uint8, CUDA) -> int64 [n] (bit pattern of u64)."""
     n, L, stride = _keys_2d(keys)
     out = _out(n, 1, keys.device, out)
-    _check(lib().pdht_city64_batch_dev(_dptr(keys), stride, L, n, _dptr(out), _stream_ptr(stream)),
-           "pdht_city64_batch_dev")
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_city64_batch_dev(_dptr(keys), stride, L, n, _dptr(out), g.stream),
+               "pdht_city64_batch_dev")
     return out
 
 
 def city64_seeds_batch(keys, seed0: int, seed1: int, out=None, stream=None):
     n, L, stride = _keys_2d(keys)
     out = _out(n, 1, keys.device, out)
-    _check(lib().pdht_city64_seeds_batch_dev(_dptr(keys), stride, L, n, seed0, seed1, _dptr(out),
-                                             _stream_ptr(stream)), "pdht_city64_seeds_batch_dev")
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_city64_seeds_batch_dev(_dptr(keys), stride, L, n, seed0, seed1, _dptr(out),
+                                                 g.stream), "pdht_city64_seeds_batch_dev")
     return out
 
 
@@ -285,71 +378,77 @@ def city64_seed_batch(keys, seed: int, out=None, stream=None):
 
 
 def _check_var(data, offsets):
+    """(n, nbytes): nbytes = the data buffer's size, the bound of the key
+    bytes the batch spans (sizes the kernel's LDS window; never addresses)."""
     torch = _torch()
     if data.dtype != torch.uint8 or not data.is_cuda or not data.is_contiguous():
         raise ValueError("data must be a contiguous CUDA uint8 tensor")
-    if offsets.dtype != torch.int64 or not offsets.is_cuda or not offsets.is_contiguous():
-        raise ValueError("offsets must be a contiguous CUDA int64 tensor of n+1 entries")
-    # the buffer size bounds the key bytes: lets the kernel size its window
-    # for the mean key length (pdht_hip_set_var_bytes_hint, one call)
-    lib().pdht_hip_set_var_bytes_hint(data.numel())
-    return offsets.numel() - 1
+    _need(offsets, "offsets", torch.int64, data.device)
+    if offsets.dim() != 1 or offsets.numel() < 1:
+        raise ValueError("offsets must be a 1-D int64 tensor of n+1 entries")
+    return offsets.numel() - 1, data.numel()
 
 
 def city64_var_batch(data, offsets, out=None, stream=None):
-    n = _check_var(data, offsets)
+    n, nb = _check_var(data, offsets)
     out = _out(n, 1, data.device, out)
-    _check(lib().pdht_city64_batch_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
-                                           _stream_ptr(stream)), "pdht_city64_batch_var_dev")
+    with _on(data.device, stream) as g:
+        _check(lib().pdht_city64_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
+               "pdht_city64_batch_var_dev")
     return out
 
 
 def city128_batch(keys, out=None, stream=None):
     n, L, stride = _keys_2d(keys)
     out = _out(n, 2, keys.device, out)
-    _check(lib().pdht_city128_batch_dev(_dptr(keys), stride, L, n, _dptr(out), _stream_ptr(stream)),
-           "pdht_city128_batch_dev")
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_city128_batch_dev(_dptr(keys), stride, L, n, _dptr(out), g.stream),
+               "pdht_city128_batch_dev")
     return out
 
 
 def city128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
     n, L, stride = _keys_2d(keys)
     out = _out(n, 2, keys.device, out)
-    _check(lib().pdht_city128_seed_batch_dev(_dptr(keys), stride, L, n, seed[0], seed[1], _dptr(out),
-                                             _stream_ptr(stream)), "pdht_city128_seed_batch_dev")
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_city128_seed_batch_dev(_dptr(keys), stride, L, n, seed[0], seed[1], _dptr(out),
+                                                 g.stream), "pdht_city128_seed_batch_dev")
     return out
 
 
 def city128_var_batch(data, offsets, out=None, stream=None):
-    n = _check_var(data, offsets)
+    n, nb = _check_var(data, offsets)
     out = _out(n, 2, data.device, out)
-    _check(lib().pdht_city128_batch_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
-                                            _stream_ptr(stream)), "pdht_city128_batch_var_dev")
+    with _on(data.device, stream) as g:
+        _check(lib().pdht_city128_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
+               "pdht_city128_batch_var_dev")
     return out
 
 
 def citycrc128_batch(keys, out=None, stream=None):
     n, L, stride = _keys_2d(keys)
     out = _out(n, 2, keys.device, out)
-    _check(lib().pdht_citycrc128_batch_dev(_dptr(keys), stride, L, n, _dptr(out),
-                                           _stream_ptr(stream)), "pdht_citycrc128_batch_dev")
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_citycrc128_batch_dev(_dptr(keys), stride, L, n, _dptr(out), g.stream),
+               "pdht_citycrc128_batch_dev")
     return out
 
 
 def citycrc128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
     n, L, stride = _keys_2d(keys)
     out = _out(n, 2, keys.device, out)
-    _check(lib().pdht_citycrc128_seed_batch_dev(_dptr(keys), stride, L, n, seed[0], seed[1],
-                                                _dptr(out), _stream_ptr(stream)),
-           "pdht_citycrc128_seed_batch_dev")
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_citycrc128_seed_batch_dev(_dptr(keys), stride, L, n, seed[0], seed[1],
+                                                    _dptr(out), g.stream), "pdht_citycrc128_seed_batch_dev")
     return out
 
 
 def citycrc128_var_batch(data, offsets, out=None, stream=None):
-    n = _check_var(data, offsets)
+    n, nb = _check_var(data, offsets)
     out = _out(n, 2, data.device, out)
-    _check(lib().pdht_citycrc128_batch_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
-                                               _stream_ptr(stream)), "pdht_citycrc128_batch_var_dev")
+    with _on(data.device, stream) as g:
+        _check(lib().pdht_citycrc128_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out),
+                                                   g.stream), "pdht_citycrc128_batch_var_dev")
     return out
 
 
@@ -358,29 +457,44 @@ def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=
     """Fused pdht_hash (hash.c:25-30) over keys [n, keysize] (packed, CUDA).
 
     Returns (mbits int64[n], ptindex int32[n] | None, rank int32[n] | None);
-    if `hist` (int64[nranks], CUDA) is given, per-rank counts are added to it.
-    `out` = a previous return value to reuse its tensors.
+    if `hist` (int64[>= nranks], CUDA) is given, per-rank counts are added to it.
+    `out` = a previous return value (same n) to reuse its tensors.
     """
     torch = _torch()
     n, L, stride = _keys_2d(keys)
     if stride != L:
         raise ValueError("place_batch needs packed keys")
+    dev = keys.device
+    if hist is not None:
+        _need(hist, "hist", torch.int64, dev, numel=nranks)
     if out is not None:
         mb, pt, rk = out
+        _need(mb, "out[0] (mbits)", torch.int64, dev, shape=(n,))
+        if pt is not None:
+            _need(pt, "out[1] (ptindex)", torch.int32, dev, shape=(n,))
+        if rk is not None:
+            _need(rk, "out[2] (rank)", torch.int32, dev, shape=(n,))
     else:
-        mb = torch.empty(n, dtype=torch.int64, device=keys.device)
-        pt = torch.empty(n, dtype=torch.int32, device=keys.device) if ptindex else None
-        rk = torch.empty(n, dtype=torch.int32, device=keys.device) if rank else None
-    _check(lib().pdht_place_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(mb),
-                                      _dptr(pt) if pt is not None else None,
-                                      _dptr(rk) if rk is not None else None, 4,
-                                      _dptr(hist) if hist is not None else None,
-                                      _stream_ptr(stream)), "pdht_place_batch_dev")
+        mb = torch.empty(n, dtype=torch.int64, device=dev)
+        pt = torch.empty(n, dtype=torch.int32, device=dev) if ptindex else None
+        rk = torch.empty(n, dtype=torch.int32, device=dev) if rank else None
+    with _on(dev, stream) as g:
+        _check(lib().pdht_place_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(mb), _opt(pt), _opt(rk), 4,
+                                          _opt(hist), g.stream), "pdht_place_batch_dev")
     return mb, pt, rk
 
 
 def bucket_workspace_bytes(n: int, nranks: int) -> int:
     return lib().pdht_bucket_workspace_bytes(n, nranks)
+
+
+def _workspace(workspace, n, nranks, dev):
+    torch = _torch()
+    need = lib().pdht_bucket_workspace_bytes(n, nranks)
+    if workspace is None:
+        return torch.empty(max(need, 1), dtype=torch.uint8, device=dev), need
+    _need(workspace, "workspace", torch.uint8, dev, numel=need)
+    return workspace, workspace.numel()
 
 
 def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=True,
@@ -389,36 +503,38 @@ def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=
     counting sort of packed keys [n, L] by rank = CityHash64 % nranks.
 
     Returns (keys_out [n, L] | None, mbits int64[n], ptindex int32[n] | None,
-    index int64[n] | None, offsets int64[nranks+1]); bucket r is rows
-    offsets[r]:offsets[r+1], keys in original order.  `out` = a previous
-    return value to reuse its tensors; `workspace` = a uint8 CUDA tensor of at
-    least bucket_workspace_bytes(n, nranks) bytes (allocated per call if None).
+    index int32[n] (unsigned original positions) | None, offsets
+    int64[nranks+1]); bucket r is rows offsets[r]:offsets[r+1], keys in
+    original order.  `out` = a previous return value (same n, L, nranks) to
+    reuse its tensors; `workspace` = a uint8 CUDA tensor of at least
+    bucket_workspace_bytes(n, nranks) bytes (allocated per call if None).
     """
     torch = _torch()
     n, L, stride = _keys_2d(keys)
     if stride != L:
         raise ValueError("bucket_batch needs packed keys")
     dev = keys.device
-    ws_bytes = lib().pdht_bucket_workspace_bytes(n, nranks)
-    if workspace is None:
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    else:
-        ws = workspace
-        if ws.numel() * ws.element_size() < ws_bytes:
-            raise ValueError(f"workspace smaller than {ws_bytes} bytes")
-        ws_bytes = ws.numel() * ws.element_size()
+    ws, ws_bytes = _workspace(workspace, n, nranks, dev)
     if out is not None:
         ko, mb, pt, ix, offs = out
+        if ko is not None:
+            _need(ko, "out[0] (keys)", torch.uint8, dev, shape=(n, L))
+        _need(mb, "out[1] (mbits)", torch.int64, dev, shape=(n,))
+        if pt is not None:
+            _need(pt, "out[2] (ptindex)", torch.int32, dev, shape=(n,))
+        if ix is not None:
+            _need(ix, "out[3] (index)", torch.int32, dev, shape=(n,))
+        _need(offs, "out[4] (offsets)", torch.int64, dev, shape=(nranks + 1,))
     else:
-        ko = torch.empty_like(keys) if with_keys else None
+        ko = torch.empty_like(keys, memory_format=torch.contiguous_format) if with_keys else None
         mb = torch.empty(n, dtype=torch.int64, device=dev)
         pt = torch.empty(n, dtype=torch.int32, device=dev) if with_ptindex else None
-        ix = torch.empty(n, dtype=torch.int64, device=dev) if with_index else None
+        ix = torch.empty(n, dtype=torch.int32, device=dev) if with_index else None
         offs = torch.empty(nranks + 1, dtype=torch.int64, device=dev)
-    p = lambda t: _dptr(t) if t is not None else None  # noqa: E731
-    _check(lib().pdht_bucket_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(ws), ws_bytes, p(ko),
-                                       _dptr(mb), p(pt), p(ix), _dptr(offs), _stream_ptr(stream)),
-           "pdht_bucket_batch_dev")
+    with _on(dev, stream) as g:
+        _check(lib().pdht_bucket_batch_dev(_dptr(keys), L, n, nptes, nranks, _dptr(ws), ws_bytes, _opt(ko),
+                                           _dptr(mb), _opt(pt), _opt(ix), _dptr(offs), g.stream),
+               "pdht_bucket_batch_dev")
     return ko, mb, pt, ix, offs
 
 
@@ -445,24 +561,22 @@ def bucket_records(keys, nranks: int, *, msg_type: int = PDHT_PUT, src_rank: int
         raise ValueError("bucket_records needs packed keys")
     dev = keys.device
     rb = bucket_record_bytes(L)
-    ws_bytes = lib().pdht_bucket_workspace_bytes(n, nranks)
-    if workspace is None:
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    else:
-        ws = workspace
-        if ws.numel() * ws.element_size() < ws_bytes:
-            raise ValueError(f"workspace smaller than {ws_bytes} bytes")
-        ws_bytes = ws.numel() * ws.element_size()
+    ws, ws_bytes = _workspace(workspace, n, nranks, dev)
     if out is not None:
         rec, offs = out
+        _need(rec, "out[0] (records)", torch.uint8, dev, shape=(n, rb))
+        if rec.data_ptr() % 8:
+            raise ValueError("records must be 8-byte aligned")
+        _need(offs, "out[1] (offsets)", torch.int64, dev, shape=(nranks + 1,))
     else:
         # int64 storage keeps the records 8-byte aligned
         rec = torch.empty(max(n * rb // 8, 1), dtype=torch.int64, device=dev).view(torch.uint8)[: n * rb]
         rec = rec.view(n, rb)
         offs = torch.empty(nranks + 1, dtype=torch.int64, device=dev)
-    _check(lib().pdht_bucket_records_dev(_dptr(keys), L, n, nranks, msg_type, src_rank, ht_index, _dptr(ws),
-                                         ws_bytes, _dptr(rec), _dptr(offs), _stream_ptr(stream)),
-           "pdht_bucket_records_dev")
+    with _on(dev, stream) as g:
+        _check(lib().pdht_bucket_records_dev(_dptr(keys), L, n, nranks, msg_type, src_rank, ht_index,
+                                             _dptr(ws), ws_bytes, _dptr(rec), _dptr(offs), g.stream),
+               "pdht_bucket_records_dev")
     return rec, offs
 
 
@@ -482,18 +596,25 @@ def splitmix64_fill(seed: int, first: int, nwords: int, out=None, device="cuda",
     torch = _torch()
     if out is None:
         out = torch.empty(nwords, dtype=torch.int64, device=device)
-    _check(lib().pdht_hip_splitmix64_fill_dev(seed, first, nwords, _dptr(out), _stream_ptr(stream)),
-           "pdht_hip_splitmix64_fill_dev")
+    else:
+        _need(out, "out", torch.int64, out.device, numel=nwords)
+    with _on(out.device, stream) as g:
+        _check(lib().pdht_hip_splitmix64_fill_dev(seed, first, nwords, _dptr(out), g.stream),
+               "pdht_hip_splitmix64_fill_dev")
     return out
 
 
 def read_stream(buf, nt: bool = False, out=None, stream=None):
     """HBM read-bandwidth calibration: XOR-fold of a CUDA buffer (16-B multiple)."""
     torch = _torch()
+    if not buf.is_contiguous():
+        raise ValueError("buf must be contiguous")
     if out is None:
         out = torch.zeros(1, dtype=torch.int64, device=buf.device)
-    _check(lib().pdht_hip_read_stream_dev(_dptr(buf), buf.numel() * buf.element_size(), int(nt),
-                                          _dptr(out), _stream_ptr(stream)), "pdht_hip_read_stream_dev")
+    _need(out, "out", torch.int64, buf.device, numel=1)
+    with _on(buf.device, stream) as g:
+        _check(lib().pdht_hip_read_stream_dev(_dptr(buf), buf.numel() * buf.element_size(), int(nt),
+                                              _dptr(out), g.stream), "pdht_hip_read_stream_dev")
     return out
 
 
@@ -503,31 +624,70 @@ def key_stream(keys, out=None, stream=None):
     n = keys.shape[0]
     if keys.dim() != 2 or keys.shape[1] != 64 or keys.dtype != torch.uint8 or not keys.is_contiguous():
         raise PdhtError("key_stream takes a contiguous (n, 64) uint8 tensor")
-    if out is None:
-        out = torch.empty(n, dtype=torch.int64, device=keys.device)
-    _check(lib().pdht_hip_key_stream_dev(_dptr(keys), n, _dptr(out), _stream_ptr(stream)),
-           "pdht_hip_key_stream_dev")
+    out = _out(n, 1, keys.device, out)
+    with _on(keys.device, stream) as g:
+        _check(lib().pdht_hip_key_stream_dev(_dptr(keys), n, _dptr(out), g.stream), "pdht_hip_key_stream_dev")
     return out
 
 
 def key_stream_var(data, offsets, out=None, stream=None):
     """Calibration: the variable-length kernel's data movement with an XOR fold."""
-    n = _check_var(data, offsets)
+    n, nb = _check_var(data, offsets)
     out = _out(n, 1, data.device, out)
-    _check(lib().pdht_hip_key_stream_var_dev(_dptr(data), _dptr(offsets), n, _dptr(out),
-                                             _stream_ptr(stream)), "pdht_hip_key_stream_var_dev")
+    with _on(data.device, stream) as g:
+        _check(lib().pdht_hip_key_stream_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
+               "pdht_hip_key_stream_var_dev")
     return out
 
 
 def mixed_lengths(seed: int, first: int, n: int, lo: int, hi: int, device="cuda", stream=None):
     torch = _torch()
     out = torch.empty(n, dtype=torch.int64, device=device)
-    _check(lib().pdht_hip_mixed_lengths_dev(seed, first, n, lo, hi, _dptr(out), _stream_ptr(stream)),
-           "pdht_hip_mixed_lengths_dev")
+    with _on(out.device, stream) as g:
+        _check(lib().pdht_hip_mixed_lengths_dev(seed, first, n, lo, hi, _dptr(out), g.stream),
+               "pdht_hip_mixed_lengths_dev")
     return out
 
 
 # ------------------------------------------------------- host batch API ---
+# Host buffers: numpy arrays or CPU torch tensors (pinned ones take the
+# zero-copy path).  Everything is checked before C sees it: dtype,
+# C-contiguity and size, so a strided view or a short `out` raises instead
+# of producing wrong digests or writing past a host buffer.
+def _host_arr(a, name, dtype, shape=None, numel=None):
+    """numpy array or CPU torch tensor of `dtype` (numpy dtype), C-contiguous."""
+    if isinstance(a, np.ndarray):
+        if a.dtype != dtype:
+            raise ValueError(f"{name} must be {np.dtype(dtype)}, got {a.dtype}")
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError(f"{name} must be C-contiguous")
+        shp, size = a.shape, a.size
+    else:
+        torch = _torch()
+        if not isinstance(a, torch.Tensor) or a.is_cuda:
+            raise ValueError(f"{name} must be a numpy array or a CPU torch tensor")
+        tdt = {np.dtype(np.uint8): torch.uint8, np.dtype(np.uint64): torch.int64,
+               np.dtype(np.uint32): torch.int32}[np.dtype(dtype)]
+        if a.dtype not in (tdt, {torch.int64: torch.uint64, torch.int32: torch.uint32}.get(tdt, tdt)):
+            raise ValueError(f"{name} must be {tdt}, got {a.dtype}")
+        if not a.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        shp, size = tuple(a.shape), a.numel()
+    if shape is not None and tuple(shp) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(shp)}")
+    if numel is not None and size < numel:
+        raise ValueError(f"{name} must hold >= {numel} elements, got {size}")
+    return a
+
+
+def _host_keys(keys):
+    """Host keys [n, L] uint8, C-contiguous (packed rows)."""
+    _host_arr(keys, "keys", np.uint8)
+    if len(keys.shape) != 2:
+        raise ValueError("keys must be 2-D [n, keylen]")
+    return tuple(keys.shape)
+
+
 def _np_keys(keys: np.ndarray):
     if keys.dtype != np.uint8 or keys.ndim != 2 or not keys.flags["C_CONTIGUOUS"]:
         raise ValueError("keys must be a C-contiguous uint8 array [n, keylen]")
@@ -543,44 +703,58 @@ def _host_ptr(a):
 
 def city64_batch_host(keys, out=None, device: int = 0):
     """Host-resident keys (numpy uint8 [n, L] or pinned CPU tensor) -> uint64 [n]."""
-    n, L = keys.shape
+    n, L = _host_keys(keys)
     if out is None:
         out = np.empty(n, dtype=np.uint64)
+    _host_arr(out, "out", np.uint64, numel=n)
     _check(lib().pdht_city64_batch_host(_host_ptr(keys), L, n, _host_ptr(out), device),
            "pdht_city64_batch_host")
     return out
 
 
-def city64_var_batch_host(data: np.ndarray, offsets: np.ndarray, out=None, device: int = 0):
-    n = offsets.size - 1
-    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+def city64_var_batch_host(data, offsets, out=None, device: int = 0):
+    _host_arr(data, "data", np.uint8)
+    offsets = _host_arr(offsets, "offsets", np.uint64)
+    n = offsets.size - 1 if isinstance(offsets, np.ndarray) else offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets must hold n+1 entries")
+    if n:
+        last = int(offsets[-1])
+        nbytes = data.nbytes if isinstance(data, np.ndarray) else data.numel()
+        if last > nbytes or int(offsets[0]) > last:
+            raise ValueError(f"offsets reach byte {last}, data holds {nbytes}")
     if out is None:
         out = np.empty(n, dtype=np.uint64)
-    _check(lib().pdht_city64_batch_var_host(_host_ptr(data), _host_ptr(offsets), n, _host_ptr(out),
-                                            device), "pdht_city64_batch_var_host")
+    _host_arr(out, "out", np.uint64, numel=n)
+    _check(lib().pdht_city64_batch_var_host(_host_ptr(data), _host_ptr(offsets), n, _host_ptr(out), device),
+           "pdht_city64_batch_var_host")
     return out
 
 
 def citycrc128_batch_host(keys, out=None, device: int = 0):
-    n, L = keys.shape
+    n, L = _host_keys(keys)
     if out is None:
         out = np.empty((n, 2), dtype=np.uint64)
+    _host_arr(out, "out", np.uint64, numel=2 * n)
     _check(lib().pdht_citycrc128_batch_host(_host_ptr(keys), L, n, _host_ptr(out), device),
            "pdht_citycrc128_batch_host")
     return out
 
 
-def place_batch_host(keys: np.ndarray, nptes: int, nranks: int, device: int = 0, out=None):
+def place_batch_host(keys, nptes: int, nranks: int, device: int = 0, out=None):
     """Host-resident fused placement; `out` = (mbits uint64[n], ptindex
     uint32[n], rank uint32[n]) host arrays to fill (pinned ones, with pinned
     keys, take the zero-copy path)."""
-    n, L = _np_keys(keys)
+    n, L = _host_keys(keys)
     if out is not None:
         mb, pt, rk = out
     else:
         mb = np.empty(n, dtype=np.uint64)
         pt = np.empty(n, dtype=np.uint32)
         rk = np.empty(n, dtype=np.uint32)
+    _host_arr(mb, "mbits", np.uint64, numel=n)
+    _host_arr(pt, "ptindex", np.uint32, numel=n)
+    _host_arr(rk, "rank", np.uint32, numel=n)
     _check(lib().pdht_place_batch_host(_host_ptr(keys), L, n, nptes, nranks, _host_ptr(mb),
                                        _host_ptr(pt), _host_ptr(rk), 4, device),
            "pdht_place_batch_host")

@@ -232,7 +232,7 @@ __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW wo
 // so the KPL atomics go out back to back (group g sees the increments of the
 // groups before it) and a single wait precedes the shuffles that hand every
 // lane its leader's base: two LDS round trips per tile instead of two per
-// group (rank_groups_serial).
+// group (the r01 form).
 template <int KPL>
 __device__ __forceinline__ void rank_groups(u32 *myrun, const u32 (&rr)[KPL], u32 q0, u32 tn,
                                             u32 nbits, u32 (&lp)[KPL]) {
@@ -250,24 +250,6 @@ __device__ __forceinline__ void rank_groups(u32 *myrun, const u32 (&rr)[KPL], u3
   }
 #pragma unroll
   for (int g = 0; g < KPL; ++g) lp[g] = (u32)__shfl((int)base[g], (int)(al[g] >> 8)) + (al[g] & 0xffu);
-}
-
-// The same, one group at a time (two LDS round trips per group).
-template <int KPL>
-__device__ __forceinline__ void rank_groups_serial(u32 *myrun, const u32 (&rr)[KPL], u32 q0, u32 tn,
-                                                   u32 nbits, u32 (&lp)[KPL]) {
-  const u32 lane = threadIdx.x & 63;
-  const u64 below = (1ull << lane) - 1;
-#pragma unroll
-  for (int g = 0; g < KPL; ++g) {
-    const bool valid = q0 + g * 64 < tn;
-    const u64 same = same_bucket_lanes(valid, rr[g], nbits);
-    const u32 ahead = (u32)__builtin_popcountll(same & below);
-    lp[g] = valid ? myrun[rr[g]] + ahead : 0;
-    wave_lds_sync();
-    if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
-    wave_lds_sync();
-  }
 }
 
 template <int L>
@@ -296,24 +278,22 @@ __device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L
 // ------------------------------------------------------------- outputs ---
 // Where a bucketed key goes; slot = its position in the bucketed batch.
 // OutSoA (pdht_bucket_batch_dev): separate arrays, each but mbits optional.
-// NT: non-temporal stores (A/B, variant 59).
-template <bool NT = false>
-struct OutSoAT {
+struct OutSoA {
   static constexpr bool kPair8 = false;
   uint8_t *keys;
   u64 *mbits;
   u32 *ptindex;
-  u64 *index;
+  u32 *index;
   FastMod pt;
   u32 L;
   __device__ __forceinline__ void meta(u64 slot, u64 h, u64 i) const {
-    st<NT>(h, mbits + slot);
-    if (ptindex) st<NT>((u32)pt.mod(h), ptindex + slot);
-    if (index) st<NT>(i, index + slot);
+    mbits[slot] = h;
+    if (ptindex) ptindex[slot] = (u32)pt.mod(h);
+    if (index) index[slot] = (u32)i;
   }
   __device__ __forceinline__ bool has_keys() const { return keys != nullptr; }
   __device__ __forceinline__ void key8(u64 slot, int c, u64 v) const {  // key bytes [8c, 8c+8)
-    st<NT>(v, reinterpret_cast<u64 *>(keys + slot * L + 8 * c));
+    *reinterpret_cast<u64 *>(keys + slot * L + 8 * c) = v;
   }
   template <int LL>
   __device__ __forceinline__ void key_row(u64 slot, const RegReader<LL / 4> &k) const {
@@ -323,7 +303,6 @@ struct OutSoAT {
     copy_row(keys + slot * L, src, L);
   }
 };
-typedef OutSoAT<false> OutSoA;
 
 // OutRec (pdht_bucket_records_dev): one wire record per key, laid out as the
 // MPI variant's request message (message_t, libmpipdht/pdht.h:120-127) with
@@ -368,39 +347,6 @@ struct OutRec {
   }
 };
 
-// Tuning only (pdht_hip_set_phase_counters): shader-clock cycles per phase of
-// a scatter kernel, summed over workgroups.  Marks sit right after barriers,
-// so thread 0's clock stands for the workgroup's.  out == nullptr: off (one
-// scalar branch per mark).
-// ON = false (production instantiations): every member is a no-op.
-template <bool ON>
-struct PhaseClock {
-  u64 *out;
-  u64 last = 0;
-  u64 acc[6] = {0, 0, 0, 0, 0, 0};
-  u64 tiles = 0;
-  __device__ __forceinline__ explicit PhaseClock(u64 *o) : out(o) {
-    if (ON && out) last = __builtin_amdgcn_s_memtime();
-  }
-  __device__ __forceinline__ void tile() {
-    if (ON) ++tiles;
-  }
-  __device__ __forceinline__ void mark(int k) {
-    if (ON && out) {
-      const u64 now = __builtin_amdgcn_s_memtime();
-      acc[k] += now - last;
-      last = now;
-    }
-  }
-  __device__ __forceinline__ void flush() {
-    if (ON && out && threadIdx.x == 0) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) atomicAdd(reinterpret_cast<unsigned long long *>(out + k), acc[k]);
-      atomicAdd(reinterpret_cast<unsigned long long *>(out + 8), tiles);
-    }
-  }
-};
-
 // ------------------------------------------------------ staged scatter ---
 // Tile = 4 waves x 16 groups x 64 lanes = 4096 keys; wave w owns the
 // contiguous quarter [w*1024, (w+1)*1024).
@@ -412,24 +358,22 @@ struct PhaseClock {
 //   D: thread j takes staged entry j -> global slot delta[r] + j: mbits,
 //      ptindex and index stores are runs of consecutive lanes;
 //   E: the keys, 8 bytes at a time, through the same staging buffer.
-// Shapes tried (r01, tools/gpu_session.sh bench_bucket@v): 8x16 and 8x8 tiles,
-// 4x8, slots of D kept in LDS, tile starts prefetched with the keys -- all
-// 8-45 % slower than this one on 16M x 8-B keys, 1024 ranks.
+// Shapes tried (r01): 8x16 and 8x8 tiles, 4x8, slots of D kept in LDS, tile
+// starts prefetched with the keys -- all 8-45 % slower than this one on 16M x
+// 8-B keys, 1024 ranks.
 constexpr int kStW = 4, kStKPL = 16;
 constexpr u32 kStTile = kStW * kStKPL * 64;
 constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL) {
   return (size_t)W * KPL * 64 * 10 + (size_t)W * nranks * 4 + (size_t)nranks * 4;
 }
-// DBG (timing-only builds, tools/bucketbench.py; results are wrong): bit 0 =
-// identity ranking, 1 = no staging writes, 2 = no mbits/ptindex/index stores,
-// 3 = no key stores, 4 = one ballot round instead of ceil(log2 nranks), 5 =
-// branch-free clamped stores (correct results; A/B of the store form).
-// W waves x KPL groups per tile (default 4 x 16 = 4096 keys).
-template <int L, class Out, bool BATCHED_RANK = true, int DBG = 0, bool PROF = false, int W = kStW,
-          int KPL = kStKPL>
+// Per-entry branches around the stores measured 12 % faster than clamped
+// branch-free stores (r01), although the branch-free form has no SGPR spills:
+// the compiler then batches each array's stores, and the store order changes
+// how the runs meet in L2.
+template <int L, class Out, int W = kStW, int KPL = kStKPL>
 __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, u32 nbits, TileStarts ts, u64 ntiles,
-    Out out, u64 *__restrict__ prof) {
+    Out out) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                              // [kTile]
@@ -442,12 +386,10 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
   u32 *myrun = run + wave * nranks;
   const u32 per = (nranks + kB - 1) / kB;
   const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
-  PhaseClock<PROF> pc(prof);
   for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kTile;
     const u32 tn = (u32)min((u64)kTile, n - tbase);
-    pc.tile();
     for (u32 j = threadIdx.x; j < W * nranks; j += kB) run[j] = 0;
     const u32 q0 = wave * kSub + lane;
     RegReader<L / 4> kr[KPL];
@@ -461,17 +403,10 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
       rr[g] = (u32)rk.mod(h[g]);
     }
     __syncthreads();
-    pc.mark(0);
 #pragma unroll
-    for (int g = 0; g < KPL; ++g) {
-      if constexpr (!(DBG & 32)) {
-        if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
-      } else {
-        atomicAdd(&myrun[rr[g]], q0 + g * 64 < tn ? 1u : 0u);  // no branch
-      }
-    }
+    for (int g = 0; g < KPL; ++g)
+      if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
     __syncthreads();
-    pc.mark(1);
     u32 s = 0;
     for (u32 r = rb0; r < rb1; ++r)
 #pragma unroll
@@ -487,24 +422,15 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
       }
     }
     __syncthreads();
-    pc.mark(2);
     u32 lp[KPL];
-    if constexpr (DBG & 1) {
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) lp[g] = q0 + g * 64;
-    } else if constexpr (BATCHED_RANK) {
-      rank_groups<KPL>(myrun, rr, q0, tn, (DBG & 16) ? 1u : nbits, lp);
-    } else {
-      rank_groups_serial<KPL>(myrun, rr, q0, tn, nbits, lp);
-    }
+    rank_groups<KPL>(myrun, rr, q0, tn, nbits, lp);
 #pragma unroll
     for (int g = 0; g < KPL; ++g)
-      if (!(DBG & 2) && q0 + g * 64 < tn) {
+      if (q0 + g * 64 < tn) {
         stage[lp[g]] = h[g];
         sidx[lp[g]] = (uint16_t)(q0 + g * 64);
       }
     __syncthreads();
-    pc.mark(3);
     constexpr int kPer = kTile / kB;
     u32 gp[kPer];
     if constexpr (Out::kPair8 && L == 8) {
@@ -529,61 +455,34 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
         if (j < tn) out.tail8(gp[jj], hv[jj], stage[j]);
       }
       __syncthreads();
-      pc.mark(5);
       continue;
     }
-    // Entries past a partial tile's end repeat its last entry (the same bytes
-    // to the same slot): no per-entry branches, whose exec masks the
-    // compiler would otherwise keep in SGPRs (and spill) across the unrolled
-    // stores.
-    // Per-entry branches around the stores measured 12 % faster than clamped
-    // branch-free stores (DBG bit 5, variant 58), although the branch-free
-    // form has no SGPR spills (48 v_readlane instead of 712 in the phase):
-    // the compiler then batches each array's stores, and the store order
-    // changes how the runs meet in L2.
-    if constexpr (!(DBG & 32)) {
 #pragma unroll
-      for (int jj = 0; jj < kPer; ++jj) {
-        const u32 j = jj * kB + threadIdx.x;
-        if (j < tn) {
-          const u64 hv = stage[j];
-          gp[jj] = delta[(u32)rk.mod(hv)] + j;
-          out.meta(gp[jj], hv, tbase + sidx[j]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int jj = 0; jj < kPer; ++jj) {
-        const u32 j = min(jj * kB + threadIdx.x, tn - 1);
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 j = jj * kB + threadIdx.x;
+      if (j < tn) {
         const u64 hv = stage[j];
         gp[jj] = delta[(u32)rk.mod(hv)] + j;
-        if (!(DBG & 4)) out.meta(gp[jj], hv, tbase + sidx[j]);
+        out.meta(gp[jj], hv, tbase + sidx[j]);
       }
     }
-    if (out.has_keys() && !(DBG & 8)) {
+    if (out.has_keys()) {
 #pragma unroll
       for (int c = 0; c < L / 8; ++c) {
         __syncthreads();
 #pragma unroll
         for (int g = 0; g < KPL; ++g)
-          if (q0 + g * 64 < tn)
-            stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
+          if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
         __syncthreads();
 #pragma unroll
         for (int jj = 0; jj < kPer; ++jj) {
-          if constexpr (!(DBG & 32)) {
-            const u32 j = jj * kB + threadIdx.x;
-            if (j < tn) out.key8(gp[jj], c, stage[j]);
-          } else {
-            out.key8(gp[jj], c, stage[min(jj * kB + threadIdx.x, tn - 1)]);
-          }
+          const u32 j = jj * kB + threadIdx.x;
+          if (j < tn) out.key8(gp[jj], c, stage[j]);
         }
       }
     }
     __syncthreads();
-    pc.mark(5);
   }
-  pc.flush();
 }
 
 // ------------------------------------------- register scatter (no staging) ---

@@ -44,3 +44,12 @@ PDHT_API uint128 CityHashCrc128WithSeed(const char *s, size_t len, uint128 seed)
 PDHT_API void CityHashCrc256(const char *s, size_t len, uint64 *result) {
   pdht::crc256(HostReader{reinterpret_cast<const uint8_t *>(s)}, len, result);
 }
+// city.c:173-187 and :190-198 (non-static in the reference, not in city.h)
+PDHT_API uint128 WeakHashLen32WithSeeds6(uint64 w, uint64 x, uint64 y, uint64 z, uint64 a, uint64 b) {
+  return to_c(pdht::weak32(w, x, y, z, a, b));
+}
+PDHT_API uint128 WeakHashLen32WithSeeds(const char *s, uint64 a, uint64 b) {
+  const pdht::HostReader r{reinterpret_cast<const uint8_t *>(s)};
+  return to_c(pdht::weak32(pdht::fetch64(r, 0), pdht::fetch64(r, 8), pdht::fetch64(r, 16),
+                           pdht::fetch64(r, 24), a, b));
+}

@@ -3,19 +3,20 @@
 // Layout of the work:
 //   * one key per lane, 64 keys per wave, digests stored lane-contiguous
 //     (8 B or 16 B per lane -> 512 B / 1 KiB per wave-instruction);
-//   * k_fixed_direct<L>: packed keys of a compile-time length L (8/16/32/64):
-//     each lane pulls its own key with L/16 global_load_dwordx4 straight into
-//     VGPRs (a wave's 4 instructions cover one contiguous 4 KiB span), the
+//   * k_fixed_direct<L>: packed keys of a compile-time length L (8/16/32):
+//     each lane pulls its own key straight into VGPRs, U keys in flight, the
 //     algorithm runs with every offset constant-folded;
-//   * k_fixed_lds<64>: same, but the wave's 4 KiB tile arrives by 4
-//     LDS-DMA instructions (global_load_lds_dwordx4, fully contiguous 1 KiB
-//     per instruction, no VGPR staging) and each lane reads its 64-byte row
-//     back with ds_read_b128 through an XOR swizzle (conflict-free);
+//   * k_fixed_xpose64: packed 64-byte keys: the wave's contiguous 4 KiB tile
+//     arrives as 4 x 1 KiB global_load_dwordx4 (two tiles of prefetch in
+//     flight) and is transposed through a swizzled per-wave LDS image so each
+//     lane holds its own key in VGPRs;
 //   * k_window: any key length, fixed stride or offset-indexed: the wave's
 //     contiguous byte range is DMA'd into a per-wave LDS window and each lane
 //     hashes its key out of LDS with byte-aligned fetches
 //     (v_alignbyte_b32); keys that do not fit the window are read from
-//     global memory directly.
+//     global memory directly;
+//   * k_global: fixed keys too long for a 64-key window, each lane walking
+//     its own key in global memory.
 // All kernels are grid-stride persistent loops (grid ~ CUs x residency) and
 // carry no inter-workgroup communication.
 #pragma once
@@ -67,30 +68,11 @@ struct LdsReader {
 // it, i.e. wait for the next tile's prefetch on the common path too.
 typedef const __attribute__((address_space(1))) u32 gu32;
 typedef const __attribute__((address_space(1))) uint8_t gu8;
-typedef const __attribute__((address_space(1))) u32x4 gu32x4;
-template <bool A16 = false>
-struct GlobalReaderT {
+struct GlobalReader {
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
-    if constexpr (A16 && N % 16 == 0) {
-      // packed keys at a 16-B multiple stride: 16-B aligned spans (every
-      // lane alike) load as dwordx4, a quarter of the instructions
-      if ((a & 15) == 0) {
-        gu32x4 *q = reinterpret_cast<gu32x4 *>(a);
-        Words<N / 4> w;
-#pragma unroll
-        for (int j = 0; j < N / 16; ++j) {
-          const u32x4 v = q[j];
-          w.d[4 * j + 0] = v.x;
-          w.d[4 * j + 1] = v.y;
-          w.d[4 * j + 2] = v.z;
-          w.d[4 * j + 3] = v.w;
-        }
-        return w;
-      }
-    }
     gu32 *q = reinterpret_cast<gu32 *>(a & ~(uintptr_t)3);
     const u32 r = (u32)(a & 3);
     u32 raw[N / 4 + 1];
@@ -107,7 +89,6 @@ struct GlobalReaderT {
     return reinterpret_cast<gu8 *>(reinterpret_cast<uintptr_t>(p))[o];
   }
 };
-typedef GlobalReaderT<false> GlobalReader;
 
 // ------------------------------------------------------------ algorithms ---
 struct AlgoCity64 {
@@ -418,86 +399,6 @@ __global__ __launch_bounds__(BS) void k_fixed_direct(const uint8_t *__restrict__
 // groups of ds_write_b128 conflict-free.
 __device__ __forceinline__ u32 xpose_slot(u32 k, u32 c) { return 4 * k + (c ^ ((k >> 2) & 3)); }
 
-// LDS byte address of a __shared__ object (for hand-issued ds_* / M0).
-template <class T>
-__device__ __forceinline__ u32 lds_addr(const T *p) {
-  return (u32)(uintptr_t)(const __attribute__((address_space(3))) T *)(p);
-}
-
-// Row read of lane `lane`'s key from an image at LDS byte address `img`,
-// hand-issued so the compiler does not tie it to outstanding LDS-DMA (it
-// would otherwise wait vmcnt(0) on every DMA in flight, prefetch included).
-__device__ __forceinline__ void read_row_asm(u32 img, u32 lane, RegReader<16> &r) {
-  const u32 sw = (lane >> 2) & 3;
-  u32x4 v[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const u32 a = img + 16 * (4 * lane + (c ^ sw));
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v[c]) : "v"(a) : "memory");
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    r.d[4 * c + 0] = v[c].x;
-    r.d[4 * c + 1] = v[c].y;
-    r.d[4 * c + 2] = v[c].z;
-    r.d[4 * c + 3] = v[c].w;
-  }}
-
-// Variant "lds": pieces arrive by LDS-DMA (global_load_lds_dwordx4, no VGPR
-// staging); the SOURCE address is permuted so that the linear DMA image is
-// the swizzled one; the next tile's DMA is in flight while this one hashes.
-template <class Algo, class Sink>
-__global__ __launch_bounds__(kBlock) void k_fixed_lds64(const uint8_t *__restrict__ keys, u64 n,
-                                                        Algo algo, Sink sink) {
-  __shared__ __attribute__((aligned(16))) u32 tile[kWavesPerBlock][2][1024];  // 2 x 4 KiB per wave
-  __shared__ u32 lds_hist[Sink::kHist];
-  sink.lds_hist = lds_hist;
-  sink.init();
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u32 lane = threadIdx.x & 63;
-  const u64 ntiles = (n + 63) >> 6;
-  const u64 full = n >> 6;  // tiles with 64 valid keys (DMA path)
-  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-
-  auto issue = [&](u64 t, int b) {
-    const uint8_t *base = keys + (t << 12);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32 g = 64 * j + lane;               // image slot this lane fills
-      const u32 k = g >> 2, cq = g & 3;            // slot holds quarter cq ^ swz(k) of key k
-      const uint8_t *src = base + k * 64 + ((cq ^ ((k >> 2) & 3)) << 4);
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)src,
-                                       (void __attribute__((address_space(3))) *)&tile[wave][b][256 * j],
-                                       16, 0, 0);
-    }
-  };
-
-  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
-  int b = 0;
-  if (t < full) issue(t, 0);
-  for (; t < ntiles; t += nwaves) {
-    const u64 tn = t + nwaves;
-    const u64 i = (t << 6) + lane;
-    RegReader<16> r;    if (t < full) {
-      if (tn < full) {
-        issue(tn, b ^ 1);  // next tile streams in while this one hashes
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      read_row_asm(lds_addr(&tile[wave][b][0]), lane, r);
-    } else if (i < n) {
-      load_key_regs<64>(keys, i, r);
-    }
-    if (i < n) sink.put(i, algo(r, (u64)64));
-    b ^= 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sink.flush();
-}
-
 // Variant "xpose": the same transpose with register staging: each lane loads
 // 4 contiguous 16-B pieces of the NEXT tile (global_load_dwordx4, 1 KiB per
 // wave-instruction) while the current tile hashes, then writes them into the
@@ -563,76 +464,6 @@ __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restr
   sink.flush();
 }
 
-// --------------------------------------------- chunk-streamed long keys ---
-// Fixed keys too long for a 64-key LDS window (keylen > 255 B; 16-B multiple
-// length and stride, 16-B aligned rows), CityHash64 and its seeded form.  The
-// >64-byte loop (city.c:236-260) consumes a key 64 bytes at a time, so a wave
-// streams the s-th 64-byte chunk of each of its 64 keys through a 4 KiB LDS
-// image per step: 4 LDS-DMA instructions of 16 keys x 64 B (the xpose64
-// swizzle applied on the source side, as in k_fixed_lds64), double-buffered
-// so chunk s+1 is in flight while chunk s is hashed, and each lane reads its
-// row back with 4 ds_read_b128.  Step 0 is the tail [L-64, L) (tail-first
-// initialisation), steps 1..R the chunks 0..R-1.  k_global (each lane walking
-// its own key with per-lane loads) is the fallback for other lengths.
-template <class A>
-struct IsCity64Algo {
-  static constexpr bool value = std::is_same<A, AlgoCity64>::value || std::is_same<A, AlgoCity64Seeds>::value;
-};
-
-template <class Algo, class Sink, int AUX = 0>
-__global__ __launch_bounds__(kBlock) void k_fixed_chunks(const uint8_t *__restrict__ keys, u64 stride, u32 L,
-                                                         u64 n, Algo algo, Sink sink) {
-  __shared__ __attribute__((aligned(16))) u32 tile[kWavesPerBlock][2][1024];  // 2 x 4 KiB per wave
-  __shared__ u32 lds_hist[Sink::kHist];
-  sink.lds_hist = lds_hist;
-  sink.init();
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u32 lane = threadIdx.x & 63;
-  const u64 ntiles = (n + 63) >> 6;
-  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  const u32 rounds = (L - 1) >> 6;
-  // image slot g = 64j + lane holds quarter (g&3) ^ swz(k) of key k = g>>2
-  auto issue = [&](u64 t, u32 off, int b) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32 g = 64 * j + lane;
-      const u32 k = g >> 2, cq = g & 3;
-      const u64 key = min((t << 6) + k, n - 1);
-      const uint8_t *src = keys + key * stride + off + ((cq ^ ((k >> 2) & 3)) << 4);
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)src,
-                                       (void __attribute__((address_space(3))) *)&tile[wave][b][256 * j], 16, 0,
-                                       AUX);
-    }
-  };
-  for (u64 t = (u64)blockIdx.x * kWavesPerBlock + wave; t < ntiles; t += nwaves) {
-    const u64 i = (t << 6) + lane;
-    issue(t, L - 64, 0);  // the tail
-    issue(t, 0, 1);       // chunk 0
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    RegReader<16> r;
-    read_row_asm(lds_addr(&tile[wave][0][0]), lane, r);
-    LongState st;
-    city64_long_init(r.template span<64>(0), L, st);
-    for (u32 q = 0; q < rounds; ++q) {
-      const int cb = (q + 1) & 1;  // chunk q sits in buffer (q+1)&1
-      if (q + 1 < rounds) {
-        issue(t, (q + 1) << 6, cb ^ 1);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      read_row_asm(lds_addr(&tile[wave][cb][0]), lane, r);
-      const Words<16> c = r.template span<64>(0);
-      if (q == 0) st.x += c.w64(0);  // "x * k1 + Fetch64(s)" (city.c:243)
-      round64(st, c);
-    }
-    u64 h = city64_long_final(st);
-    if constexpr (std::is_same<Algo, AlgoCity64Seeds>::value) h = mix16(h - algo.s0, algo.s1);
-    if (i < n) sink.put(i, h);
-  }
-  sink.flush();
-}
-
 // --------------------------------------------------------- window kernel ---
 // Any key length.  VAR: key i = bytes[offsets[i]-obase, offsets[i+1]-obase);
 // otherwise key i = bytes[i*stride, i*stride+keylen).  WIN = LDS bytes per
@@ -678,17 +509,21 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
     // beyond WIN bytes (only in tiles of long keys) are read from global
     // memory instead (a multi-pass variant that re-staged the remainder was
     // measured slower: each extra pass is a serialised DMA round trip).
-    u64 wlo;
+    // Window bounds are ABSOLUTE addresses: wlo is the 16-B block holding the
+    // tile's first key byte, so every 16-B DMA piece below lies in a block
+    // that holds key bytes, and no piece reaches a page the keys do not
+    // touch, whatever the alignment of `bytes` (zero-copy host buffers).
+    const u64 base = (u64)(uintptr_t)bytes;
+    u64 first;
     if constexpr (VAR)
-      wlo = offsets[k0] - obase;
+      first = offsets[k0] - obase;
     else
-      wlo = k0 * stride;
-    wlo &= ~(u64)15;
-    const u64 span = whi - wlo;
+      first = k0 * stride;
+    const u64 wlo = (base + first) & ~(u64)15;
+    const u64 span = whi > first ? base + whi - wlo : 0;  // a tile of empty keys reads nothing
     const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
     // DMA the window: piece j moves 1 KiB, lane l's 16 B to LDS 1024j+16l.
-    // 16-B-aligned pieces never cross a page the key bytes do not touch.
-    const uint8_t *src = bytes + wlo;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)wlo);
 #pragma unroll
     for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
       if ((u32)j * 1024 < wbytes) {  // wave-uniform
@@ -703,8 +538,8 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
     if (valid) {
       const u64 len = end - start;
       typename Algo::Out h;
-      if (end - wlo <= wbytes)
-        h = algo(LdsReader{lds, (u32)(start - wlo)}, len);
+      if (base + end - wlo <= wbytes)
+        h = algo(LdsReader{lds, (u32)(base + start - wlo)}, len);
       else
         h = algo(GlobalReader{bytes + start}, len);
       sink.put(i, h);
@@ -719,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
 // lane walks its own key straight from global memory (GlobalReader); the
 // other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
 // bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
-template <bool VAR, class Algo, class Sink, bool A16 = false>
+template <bool VAR, class Algo, class Sink>
 __global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -738,316 +573,7 @@ __global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ b
       st = i * stride;
       len = keylen;
     }
-    sink.put(i, algo(GlobalReaderT<A16>{bytes + st}, len));
-  }
-  sink.flush();
-}
-
-// ------------------------------------------- double-buffered window kernel ---
-// Offset-indexed keys.  k_window with two LDS windows per wave: while tile t
-// hashes out of one window, the LDS-DMA of tile t+nwaves streams into the
-// other, and the offsets of tile t+2*nwaves are already on their way.  The
-// windows are two distinct __shared__ objects and the loop is unrolled by two,
-// so every LDS read names its window and the compiler's LDS-DMA wait tracking
-// (alias scopes per LDS object) only waits for the DMA into THAT window.
-// Per tile, one vector load of offsets[k0+lane] (a key's end = its right
-// neighbour's start) and one uniform load of offsets[kend].
-template <int WIN>
-struct WinGeo {
-  u64 wlo;     // 16-B aligned window start (bytes index, relative to obase)
-  u64 start;   // this lane's key
-  u64 end;
-  u32 wbytes;  // bytes staged (<= WIN)
-};
-
-template <int WIN, class Algo, class Sink, int AUX = 2>
-__global__ __launch_bounds__(kBlock) void k_window2(const uint8_t *__restrict__ bytes,
-                                                    const u64 *__restrict__ offsets, u64 obase,
-                                                    u64 n, Algo algo, Sink sink) {
-  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
-  __shared__ __attribute__((aligned(16))) u32 winA[kWavesPerBlock * (WIN / 4) + 4];
-  __shared__ __attribute__((aligned(16))) u32 winB[kWavesPerBlock * (WIN / 4) + 4];
-  __shared__ u32 lds_hist[Sink::kHist];
-  sink.lds_hist = lds_hist;
-  algo_init(algo);
-  sink.init();
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u32 lane = threadIdx.x & 63;
-  const u64 ntiles = (n + 63) >> 6;
-  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  u32 *const wa = winA + wave * (WIN / 4);
-  u32 *const wb = winB + wave * (WIN / 4);
-
-  // offsets of tile t: this lane's start, and the tile's end (uniform)
-  auto load_offs = [&](u64 t, u64 &a, u64 &hi) {
-    const u64 k0 = t << 6;
-    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
-    a = offsets[(k0 + lane < n) ? k0 + lane : n];
-    hi = offsets[kend];
-  };
-  auto geometry = [&](u64 a, u64 hi) {
-    WinGeo<WIN> g;
-    const u64 nb = __shfl_down(a, 1);
-    g.start = a - obase;
-    g.end = (lane == 63 ? hi : nb) - obase;
-    // readfirstlane returns int: widen through u32 (no sign extension)
-    const u64 a0 = (u64)(u32)__builtin_amdgcn_readfirstlane((u32)a) |
-                   ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(a >> 32)) << 32);
-    g.wlo = a0 - obase;
-    g.wlo &= ~(u64)15;
-    const u64 span = (hi - obase) - g.wlo;
-    g.wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
-    return g;
-  };
-  auto issue = [&](const WinGeo<WIN> &g, u32 *w) {
-    const uint8_t *src = bytes + g.wlo;
-#pragma unroll
-    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
-      if ((u32)j * 1024 < g.wbytes) {  // wave-uniform
-        if ((u32)j * 1024 + lane * 16 < g.wbytes)
-          __builtin_amdgcn_global_load_lds(
-              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
-              (void __attribute__((address_space(3))) *)(w + 256 * j), 16, 0, AUX);
-      }
-    }
-  };
-  // a tile's digests are stored one step late, right after the next DMA is
-  // issued: the wait at the top of a step then only covers operations issued
-  // a whole tile of hashing earlier (on CDNA a load wait also waits for every
-  // older store)
-  typename Algo::Out h{};
-  u64 hi_pend = ~0ull;  // index of the digest held in h (~0: none)
-  auto hash = [&](u64 t, const WinGeo<WIN> &g, const u32 *w) {
-    const u64 i = (t << 6) + lane;
-    hi_pend = ~0ull;
-    if (i < n) {
-      const u64 len = g.end - g.start;
-      if (g.end - g.wlo <= g.wbytes)
-        h = algo(LdsReader{w, (u32)(g.start - g.wlo)}, len);
-      else
-        h = algo(GlobalReader{bytes + g.start}, len);
-      hi_pend = i;
-    }
-  };
-  auto put_pending = [&] {
-    if (hi_pend != ~0ull) sink.put(hi_pend, h);
-  };
-
-  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
-  if (t < ntiles) {
-    u64 a, hi, an, hin;
-    load_offs(t, a, hi);
-    WinGeo<WIN> g = geometry(a, hi), gn;
-    issue(g, wa);
-    // offsets loads are unconditional (clamped tile): a conditional load
-    // merges with the old value through a register copy, and the copy waits
-    // vmcnt(0) for the DMA issued just before it
-    const u64 last = ntiles - 1;
-    load_offs(min(t + nwaves, last), an, hin);
-    // one step: hash tile t out of `cur` while tile t+nwaves streams into `nxt`
-    auto step = [&](u32 *cur, u32 *nxt) -> bool {
-      const u64 tn = t + nwaves;
-      const bool more = tn < ntiles;  // wave-uniform
-      // tile t's DMA (issued one step ago) has landed; the compiler does not
-      // order LDS reads after LDS-DMA by itself, so this wait is what makes
-      // `cur` readable (it also covers the offsets loads of the same step)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (more) {
-        gn = geometry(an, hin);
-        issue(gn, nxt);
-      }
-      put_pending();
-      if (more) load_offs(min(tn + nwaves, last), an, hin);
-      hash(t, g, cur);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // `cur` is the DMA target two tiles on
-      g = gn;
-      t = tn;
-      return more;
-    };
-    while (step(wa, wb) && step(wb, wa)) {
-    }
-    put_pending();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sink.flush();
-}
-
-// ------------------------------------------------- pipelined window kernel ---
-// k_window with the next tile's window prefetched into VGPRs (WIN/1024
-// global_load_dwordx4 per lane, contiguous 1 KiB per wave-instruction) while
-// the current tile hashes out of LDS; the prefetched pieces are written into
-// the (single) per-wave LDS window with ds_write_b128 at the top of the next
-// iteration.  Ordinary loads, so the compiler's waits stay exact (LDS-DMA
-// would make it drain every outstanding DMA before each LDS read).
-template <int WIN, bool VAR, class Algo, class Sink>
-__global__ __launch_bounds__(kBlock) void k_window_pf(const uint8_t *__restrict__ bytes,
-                                                      const u64 *__restrict__ offsets, u64 obase,
-                                                      u64 stride, u64 keylen, u64 n, Algo algo,
-                                                      Sink sink) {
-  static_assert(WIN % 1024 == 0, "window = whole 1 KiB pieces");
-  constexpr int P = WIN / 1024;
-  __shared__ __attribute__((aligned(16))) u32 win[kWavesPerBlock][WIN / 4 + 4];
-  __shared__ u32 lds_hist[Sink::kHist];
-  sink.lds_hist = lds_hist;
-  algo_init(algo);
-  sink.init();
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u32 lane = threadIdx.x & 63;
-  const u64 ntiles = (n + 63) >> 6;
-  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  u32 *lds = win[wave];
-  u32x4 *lds4 = reinterpret_cast<u32x4 *>(lds);
-
-  struct Tile {
-    u64 wlo;      // 16-B aligned window start (byte offset into `bytes`)
-    u32 wbytes;   // bytes of the window actually staged (<= WIN)
-    u64 start, end;
-  };
-  auto geometry = [&](u64 t) {
-    Tile g;
-    const u64 k0 = t << 6;
-    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
-    const u64 i = k0 + lane;
-    u64 whi;
-    if constexpr (VAR) {
-      g.wlo = (offsets[k0] - obase) & ~(u64)15;
-      whi = offsets[kend] - obase;
-      g.start = i < n ? offsets[i] - obase : 0;
-      g.end = i < n ? offsets[i + 1] - obase : 0;
-    } else {
-      g.wlo = (k0 * stride) & ~(u64)15;
-      whi = (kend - 1) * stride + keylen;
-      g.start = i * stride;
-      g.end = g.start + keylen;
-    }
-    const u64 span = whi - g.wlo;
-    g.wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
-    return g;
-  };
-  u32x4 pre[P];
-  auto prefetch = [&](const Tile &g) {
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(bytes + g.wlo) + lane;
-#pragma unroll
-    for (int j = 0; j < P; ++j)
-      if ((u32)j * 1024 + lane * 16 < g.wbytes) pre[j] = __builtin_nontemporal_load(src + 64 * j);
-  };
-
-  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
-  Tile cur{};
-  if (t < ntiles) {
-    cur = geometry(t);
-    prefetch(cur);
-  }
-  for (; t < ntiles; t += nwaves) {
-#pragma unroll
-    for (int j = 0; j < P; ++j)
-      if ((u32)j * 1024 + lane * 16 < cur.wbytes) lds4[64 * j + lane] = pre[j];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const Tile g = cur;
-    const u64 tn = t + nwaves;
-    if (tn < ntiles) {  // next tile streams in while this one hashes
-      cur = geometry(tn);
-      prefetch(cur);
-    }
-    const u64 i = (t << 6) + lane;
-    if (i < n) {
-      const u64 len = g.end - g.start;
-      typename Algo::Out h;
-      if (g.end - g.wlo <= g.wbytes)
-        h = algo(LdsReader{lds, (u32)(g.start - g.wlo)}, len);
-      else
-        h = algo(GlobalReader{bytes + g.start}, len);
-      sink.put(i, h);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();  // the window is rewritten by the next tile
-  }
-  sink.flush();
-}
-
-// ------------------------------------------------ class-sorted var keys ---
-// Cost class of a key: which code path CityHash takes (city.c:225-233) and,
-// for long keys, how many 64-byte rounds (city.c:246).
-__device__ __forceinline__ u32 len_class(u64 len) {
-  if (len <= 16) return 0;
-  if (len <= 32) return 1;
-  if (len <= 64) return 2;
-  const u64 r = (len - 1) >> 6;  // 1.. rounds
-  return r >= 4 ? 6u : (u32)(2 + r);
-}
-
-// Variable-length keys, block tiles of 256 keys.  The tile's contiguous byte
-// range is DMA'd into one LDS window shared by the block; the tile's keys are
-// counting-sorted by cost class in LDS and thread t hashes the t-th key of
-// that order, so a wave runs (mostly) one code path with one trip count
-// instead of every path its 64 lanes' lengths touch.  Digests go back to
-// their original index.  Keys not inside the window (tile bytes > WINB) are
-// read from global memory.
-template <int WINB, class Algo, class Sink>
-__global__ __launch_bounds__(kBlock) void k_var_sorted(const uint8_t *__restrict__ bytes,
-                                                       const u64 *__restrict__ offsets, u64 obase,
-                                                       u64 n, Algo algo, Sink sink) {
-  static_assert(WINB % 1024 == 0, "window = whole 1 KiB DMA pieces");
-  __shared__ __attribute__((aligned(16))) u32 win[WINB / 4 + 4];
-  __shared__ u32 s_rel[kBlock], s_len[kBlock], s_perm[kBlock], s_cnt[8];
-  __shared__ u32 lds_hist[Sink::kHist];
-  sink.lds_hist = lds_hist;
-  algo_init(algo);
-  sink.init();
-  const u32 tid = threadIdx.x;
-  const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const u32 lane = tid & 63;
-  const u64 ntiles = (n + kBlock - 1) / kBlock;
-  for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const u64 k0 = t * kBlock;
-    const u64 kend = (k0 + kBlock < n) ? k0 + kBlock : n;
-    const u64 i = k0 + tid;
-    const bool valid = i < n;
-    const u64 wlo = (offsets[k0] - obase) & ~(u64)15;
-    const u64 whi = offsets[kend] - obase;
-    const u64 span = whi - wlo;
-    const u32 wbytes = span < (u64)WINB ? (u32)span : (u32)WINB;
-    // DMA the window: pieces of 1 KiB, wave w takes pieces w, w+4, ...
-    const uint8_t *src = bytes + wlo;
-    for (u32 j = wave; j * 1024 < wbytes; j += kWavesPerBlock) {
-      if (j * 1024 + lane * 16 < wbytes)
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
-            (void __attribute__((address_space(3))) *)(win + 256 * j), 16, 0, 0);
-    }
-    // key geometry + class while the DMA is in flight
-    u32 cls = 7;
-    if (valid) {
-      const u64 st = offsets[i] - obase, en = offsets[i + 1] - obase;
-      s_rel[tid] = (u32)(st - wlo);
-      s_len[tid] = (u32)(en - st);
-      cls = len_class(en - st);
-    }
-    if (tid < 8) s_cnt[tid] = 0;
-    __syncthreads();
-    const u32 pos = atomicAdd(&s_cnt[cls], 1u);
-    __syncthreads();
-    u32 base = 0;
-#pragma unroll
-    for (u32 c = 0; c < 7; ++c) base += (c < cls) ? s_cnt[c] : 0u;
-    s_perm[base + pos] = tid;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid < kend - k0) {
-      const u32 me = s_perm[tid];
-      const u32 rel = s_rel[me], len = s_len[me];
-      typename Algo::Out h;
-      if (span <= 0xffffffffull && (u64)rel + len <= wbytes) {
-        h = algo(LdsReader{win, rel}, (u64)len);
-      } else {  // outside the window: straight from global memory
-        h = algo(GlobalReader{bytes + (offsets[k0 + me] - obase)}, (u64)len);
-      }
-      sink.put(k0 + me, h);
-    }
-    __syncthreads();  // window, perm and geometry are rewritten by the next tile
+    sink.put(i, algo(GlobalReader{bytes + st}, len));
   }
   sink.flush();
 }

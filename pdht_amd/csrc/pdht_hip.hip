@@ -34,9 +34,16 @@ static int fail(const char *fmt, const char *a = "", long long b = 0) {
     if (e_ != hipSuccess) return fail("%s (" #expr ")", hipGetErrorString(e_)); \
   } while (0)
 
+// Tuning build (libpdht_hip_tuning.so, -DPDHT_HIP_TUNING; tools/ and the
+// A/B tests only): a process-wide variant number selects an alternative
+// kernel where one exists, and the workgroups per CU can be overridden.  The
+// product library has neither: one measured-best kernel per path, no
+// process-global mutable state, no environment knobs.
+#ifdef PDHT_HIP_TUNING
 static std::atomic<int> g_variant{0};
-// Total key bytes of the next variable-length batch on this thread (0 = unknown).
-static thread_local u64 g_var_bytes_hint = 0;
+static std::atomic<int> g_per_cu{0};
+static int tuning_variant() { return g_variant.load(std::memory_order_relaxed); }
+#endif
 
 // ------------------------------------------------------- device state ---
 constexpr int kMaxDev = 64;
@@ -60,13 +67,10 @@ static int current_device(int *dev) {
 
 // Persistent grid: enough workgroups to keep every CU at `per_cu` blocks,
 // never more than the work needs.
-static int env_int(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
 static unsigned grid_for(u64 work_blocks, int per_cu, int dev) {
-  const int ovr = env_int("PDHT_HIP_BLOCKS_PER_CU", 0);  // tuning experiments only
-  if (ovr > 0) per_cu = ovr;
+#ifdef PDHT_HIP_TUNING
+  if (const int o = g_per_cu.load(std::memory_order_relaxed)) per_cu = o;
+#endif
   const u64 cap = (u64)std::max(1, g_dev[dev].cus) * per_cu;
   return (unsigned)std::max<u64>(1, std::min<u64>(work_blocks, cap));
 }
@@ -87,18 +91,19 @@ static FastMod make_fastmod(u64 d) {
 }
 
 // --------------------------------------------------------- launchers ---
-constexpr int kWinBytes = 12288;     // k_window: LDS window per wave (12 KiB)
-constexpr int kVarWinBytes = 36864;  // k_var_sorted: per 256-key tile; 4 blocks per CU
+constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wave (12 KiB)
+// Kernel tags (pdht_hip_last_kernel): the kernel and its launch shape, so a
+// profile taken of one shape (profiles/traffic_*.json) is never attributed to
+// another.
 
 // Packed 8/16/32-byte keys: each lane loads its own key (lane-adjacent rows,
 // so 8- and 16-byte keys are fully coalesced), U keys in flight per lane.
-// Defaults from tools/placebench.py (interleaved A/B): 8-B keys with
-// non-temporal stores (+26 % on fused placement), 16-B keys with
-// non-temporal loads and stores (+6-11 %).  Variants: 16 = nt loads+stores,
-// 17 = nt stores, 18 = plain.
-template <int LMAX, class Algo, class Sink>
+// tools/placebench.py (interleaved A/B, r01): 8-B keys with non-temporal
+// stores (+26 % on fused placement), 16-B keys with non-temporal loads and
+// stores (+6-11 %).
+template <class Algo, class Sink>
 static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Sink sink,
-                         hipStream_t st, int dev, u64 blocks, int variant) {
+                         hipStream_t st, int dev, u64 blocks) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt snt = NtSink<Sink>::make(sink);
   if constexpr (std::is_same<Sink, SinkPlace>::value) {
@@ -107,55 +112,38 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // run at the memory-side atomic rate (~1.3 TB/s of added bytes): 2048
     // workgroups x 1024 bins x 8 B took ~16 us of an 85-us launch; a quarter
     // as many workgroups measured +24 % (8-B keys) and +29 % (16-B keys) on
-    // 16M keys, 1024 ranks (tools/placebench.py, r01).  Variant 20 keeps the
-    // 256-thread kernel; 19 forces this one.
-    const bool wide = variant == 19 || (sink.hist && variant != 16 && variant != 17 && variant != 18 &&
-                                        variant != 20);
-    if (wide) {
-      if (keylen == 8) {
-        g_kernel = "k_fixed_direct<8,4,nt-store,1024>";
-        k_fixed_direct<8, 4, Algo, SinkNt, false, 1024>
-            <<<grid_for((blocks + 15) / 16, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
-        return;
-      }
-      if (keylen == 16) {
-        g_kernel = "k_fixed_direct<16,2,nt,1024>";
-        k_fixed_direct<16, 2, Algo, SinkNt, true, 1024>
-            <<<grid_for((blocks + 7) / 8, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
-        return;
-      }
+    // 16M keys, 1024 ranks (tools/placebench.py, r01).
+    if (sink.hist && keylen == 8) {
+      g_kernel = "k_fixed_direct<8,4,nt-store,1024>@2";
+      k_fixed_direct<8, 4, Algo, SinkNt, false, 1024>
+          <<<grid_for((blocks + 15) / 16, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+      return;
+    }
+    if (sink.hist && keylen == 16) {
+      g_kernel = "k_fixed_direct<16,2,nt,1024>@2";
+      k_fixed_direct<16, 2, Algo, SinkNt, true, 1024>
+          <<<grid_for((blocks + 7) / 8, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+      return;
     }
   }
-  if constexpr (LMAX == 8) {
-    const unsigned g = grid_for((blocks + 3) / 4, 8, dev);
-    if (variant == 16) {
-      g_kernel = "k_fixed_direct<8,4,nt>";
-      k_fixed_direct<8, 4, Algo, SinkNt, true><<<g, kBlock, 0, st>>>(k, n, algo, snt);
-    } else if (variant == 18) {
-      g_kernel = "k_fixed_direct<8,4,plain>";
-      k_fixed_direct<8, 4, Algo, Sink><<<g, kBlock, 0, st>>>(k, n, algo, sink);
-    } else {
-      g_kernel = "k_fixed_direct<8,4,nt-store>";
-      k_fixed_direct<8, 4, Algo, SinkNt, false><<<g, kBlock, 0, st>>>(k, n, algo, snt);
-    }
+  if (keylen == 8) {
+    g_kernel = "k_fixed_direct<8,4,nt-store>@8";
+    k_fixed_direct<8, 4, Algo, SinkNt, false><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(
+        k, n, algo, snt);
+  } else if (keylen == 16) {
+    g_kernel = "k_fixed_direct<16,2,nt>@8";
+    k_fixed_direct<16, 2, Algo, SinkNt, true><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(
+        k, n, algo, snt);
   } else {
-    const unsigned g = grid_for((blocks + 1) / 2, 8, dev);
-    if (keylen == 32) {
-      g_kernel = "k_fixed_direct<32,2>";
-      k_fixed_direct<32, 2, Algo, Sink><<<g, kBlock, 0, st>>>(k, n, algo, sink);
-    } else if (variant == 18 || variant == 17) {
-      g_kernel = "k_fixed_direct<16,2,plain>";
-      k_fixed_direct<16, 2, Algo, Sink><<<g, kBlock, 0, st>>>(k, n, algo, sink);
-    } else {
-      g_kernel = "k_fixed_direct<16,2,nt>";
-      k_fixed_direct<16, 2, Algo, SinkNt, true><<<g, kBlock, 0, st>>>(k, n, algo, snt);
-    }
+    g_kernel = "k_fixed_direct<32,2>@8";
+    k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                            sink);
   }
 }
 
-// Fixed-length keys: dispatch to the register-direct / LDS-transposed kernel
-// when the length is one of the specialised ones and the layout allows it,
-// else to the generic window kernel.
+// Fixed-length keys: the register-direct / LDS-transposed kernels for the
+// specialised lengths when the layout allows them, else the window kernel
+// (a 64-key tile fits 12 or 16 KiB of LDS), else per-lane global reads.
 template <class Algo, class Sink>
 static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo,
                         Sink sink, hipStream_t st) {
@@ -168,204 +156,93 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
   const bool packed = stride == keylen;
   const bool al16 = ((uintptr_t)k & 15) == 0;
   const bool al8 = ((uintptr_t)k & 7) == 0;
-  const int variant = g_variant.load(std::memory_order_relaxed);
   const u64 blocks = (n + kBlock - 1) / kBlock;
-  if (packed && keylen == 64 && al16 && variant != 3) {
-    typedef typename NtSink<Sink>::type SinkNt;
-    const SinkNt sink_nt = NtSink<Sink>::make(sink);
-    const unsigned g1 = grid_for(blocks, 8, dev), g4 = grid_for((n + 255) / 256, 4, dev);
-    switch (variant) {
-      case 2:
-        g_kernel = "k_fixed_lds64";
-        k_fixed_lds64<Algo, Sink><<<g4, kBlock, 0, st>>>(k, n, algo, sink);
-        break;
-      case 4:
-        g_kernel = "k_fixed_lds64<nt-store>";
-        k_fixed_lds64<Algo, SinkNt><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
-      case 5:
-        g_kernel = "k_fixed_direct<64,1,nt-load,nt-store>";
-        k_fixed_direct<64, 1, Algo, SinkNt, true><<<g1, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
-      case 6:
-        g_kernel = "k_fixed_direct<64,1>";
-        k_fixed_direct<64, 1, Algo, Sink, false><<<g1, kBlock, 0, st>>>(k, n, algo, sink);
-        break;
-      case 8:
-        g_kernel = "k_fixed_xpose64<nt-store>";
-        k_fixed_xpose64<Algo, SinkNt, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
-      case 9:
-        g_kernel = "k_fixed_direct<64,1,nt-store>";
-        k_fixed_direct<64, 1, Algo, SinkNt, false><<<g1, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
-      case 15:
-        g_kernel = "k_fixed_xpose64<depth2>";
-        k_fixed_xpose64<Algo, SinkNt, true, 2><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
-      case 26:
-        g_kernel = "k_fixed_xpose64<nt-load,plain-store>";
+  typedef typename NtSink<Sink>::type SinkNt;
+  const SinkNt sink_nt = NtSink<Sink>::make(sink);
+  // the CRC-table algorithms serve keys > 900 B only: window / global kernels
+  constexpr bool kShort = !HasCrcLds<Algo>::value;
+  if (kShort && packed && keylen == 64 && al16) {
+#ifdef PDHT_HIP_TUNING
+    if constexpr (kShort) {
+      if (tuning_variant() == 7) {  // one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
+        g_kernel = "k_fixed_xpose64<nt,d1>@4";
+        k_fixed_xpose64<Algo, SinkNt, true, 1><<<grid_for((n + 255) / 256, 4, dev), kBlock, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+      if (tuning_variant() == 26) {  // plain digest stores (r01: 2-6 % slower)
+        g_kernel = "k_fixed_xpose64<nt-load,plain-store,d2>@3";
         k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
             k, n, algo, sink);
-        break;
-      case 1:
-        g_kernel = "k_fixed_xpose64<plain>";
-        k_fixed_xpose64<Algo, Sink, false><<<g4, kBlock, 0, st>>>(k, n, algo, sink);
-        break;
-      case 7:
-        g_kernel = "k_fixed_xpose64<depth1>";
-        k_fixed_xpose64<Algo, SinkNt, true><<<g4, kBlock, 0, st>>>(k, n, algo, sink_nt);
-        break;
-      default:  // 0: measured fastest (tools/kbench.py): nt/nt,
-                // two tiles of prefetch in flight per wave, 3 workgroups per CU
-        g_kernel = "k_fixed_xpose64";
-        k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
-            k, n, algo, sink_nt);
-        break;
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
     }
-  } else if (packed && (keylen == 32 || keylen == 16) && al16 && variant != 3) {
-    launch_small<32>(keylen, k, n, algo, sink, st, dev, blocks, variant);
-  } else if (packed && keylen == 8 && al8 && variant != 3) {
-    launch_small<8>(keylen, k, n, algo, sink, st, dev, blocks, variant);
+#endif
+    // measured fastest (tools/kbench.py): non-temporal loads
+    // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU
+    g_kernel = "k_fixed_xpose64<nt,d2>@3";
+    if constexpr (kShort)
+      k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+          k, n, algo, sink_nt);
+  } else if (kShort && packed && (((keylen == 32 || keylen == 16) && al16) || (keylen == 8 && al8))) {
+    if constexpr (kShort) launch_small(keylen, k, n, algo, sink, st, dev, blocks);
   } else {
     const u64 tiles = (n + 63) / 64;
-    typedef typename NtSink<Sink>::type SinkNt;
     const u64 tile_bytes = 63 * (u64)stride + keylen + 16;  // a 64-key tile + alignment slack
-    if (variant == 3) {
-      g_kernel = "k_window<fixed>";
-      k_window<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, sink);
-    } else if (variant == 14) {
-      g_kernel = "k_window_pf<fixed>";
-      k_window_pf<kWinBytes, false, Algo, Sink><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, sink);
-    } else if (variant == 11) {
-      g_kernel = "k_window<fixed,nt,10224>";
-      k_window<10224, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 4, dev), kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
-    } else if (variant == 27 || (variant != 28 && tile_bytes > 16384)) {
-      // keys too long for a 64-key window (tools/longbench.py, r01)
-      // the 16-B reader measured equal to dword loads (longbench r01): variant only
-      // k_fixed_chunks (variant 32): 0.36-0.47 of peak against k_global's
-      // 0.50-0.62 on 256 B - 8 KiB keys (longbench r01): one chunk of
-      // prefetch per wave keeps fewer bytes in flight than 32 waves of
-      // per-lane loads
-      if constexpr (IsCity64Algo<Algo>::value) {
-        if (al16 && stride % 16 == 0 && keylen % 16 == 0 && keylen > 64 && variant == 32) {
-          g_kernel = "k_fixed_chunks";
-          k_fixed_chunks<Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 4, dev), kBlock, 0, st>>>(
-              k, stride, (u32)keylen, n, algo, NtSink<Sink>::make(sink));
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
-      }
-      if (al16 && stride % 16 == 0 && variant == 30) {
-        g_kernel = "k_global<fixed,a16>";
-        k_global<false, Algo, SinkNt, true><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
-            k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
-      } else {
-        g_kernel = "k_global<fixed>";
-        k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
-            k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
-      }
+    if (tile_bytes > 16384) {
+      // keys too long for a 64-key window: per-lane global reads (r01: an
+      // LDS chunk-streaming kernel measured 0.36-0.47 of peak against this
+      // kernel's 0.50-0.62 on 256 B - 8 KiB keys)
+      g_kernel = "k_global<fixed>@8";
+      k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(k, nullptr, 0, stride,
+                                                                                  keylen, n, algo, sink_nt);
     } else if (tile_bytes > kWinBytes) {
-      g_kernel = "k_window<fixed,nt,16K>";
+      g_kernel = "k_window<fixed,nt,16K>@2";
       k_window<16384, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 2, dev), kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
     } else {  // (10224 B at 4 WG/CU measured 2-4 % slower for fixed keys: longbench r01)
-      g_kernel = "k_window<fixed,nt>";
+      g_kernel = "k_window<fixed,nt,12K>@3";
       k_window<kWinBytes, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, NtSink<Sink>::make(sink));
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
     }
   }
   HIP_TRY(hipGetLastError());
   return 0;
 }
 
+// Variable-length keys.  `nbytes` = key bytes the batch spans
+// (offsets[n] - offsets[0]; 0 = unknown) sizes the LDS window for the mean
+// key length (tools/varbench.py, r01): mean <= 160 B (cfg3's 16..256 mix,
+// mean 136) -> 10224 B per wave at 4 workgroups/CU; longer -> 16 KiB at 2.
+// (Per-lane global reads measured slower than the 16 KiB window even at
+// 1-3 KiB keys: the window's DMA pulls the lines into L2 for the keys that
+// overflow it.)
 template <class Algo, class Sink>
-static int launch_var(const void *bytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
+static int launch_var(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
                       Sink sink, hipStream_t st) {
-  const u64 hint = g_var_bytes_hint;
-  g_var_bytes_hint = 0;  // one call only
   if (n == 0) return 0;
   if (!bytes || !offsets) return fail("null bytes/offsets pointer%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
   const uint8_t *b = static_cast<const uint8_t *>(bytes);
-  const int variant = g_variant.load(std::memory_order_relaxed);
-  if (variant == 10) {  // class-sorted block tiles (measured slower, kept for A/B)
-    g_kernel = "k_var_sorted";
-    k_var_sorted<kVarWinBytes, Algo, Sink><<<grid_for((n + kBlock - 1) / kBlock, 4, dev), kBlock, 0, st>>>(
-        b, offsets, obase, n, algo, sink);
+  typedef typename NtSink<Sink>::type SinkNt;
+  const SinkNt sink_nt = NtSink<Sink>::make(sink);
+  const u64 wb = ((n + 63) / 64 + 3) / 4;  // blocks of 4 wave-tiles
+  bool wide = nbytes / n > 160;
+#ifdef PDHT_HIP_TUNING
+  if (tuning_variant() == 12) wide = false;
+  if (tuning_variant() == 13) wide = true;
+#endif
+  if (wide) {
+    g_kernel = "k_window<var,nt,16K>@2";
+    k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,
+                                                                                    algo, sink_nt);
   } else {
-    typedef typename NtSink<Sink>::type SinkNt;
-    const SinkNt sink_nt = NtSink<Sink>::make(sink);
-    const u64 wb = ((n + 63) / 64 + 3) / 4;  // blocks of 4 wave-tiles
-    switch (variant) {
-      case 3:
-        g_kernel = "k_window<var>";
-        k_window<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, sink);
-        break;
-      case 12:
-        g_kernel = "k_window<var,nt,10224>";
-        k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, sink_nt);
-        break;
-      case 13:
-        g_kernel = "k_window<var,nt,16K>";
-        k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, sink_nt);
-        break;
-      case 14:
-        g_kernel = "k_window_pf<var>";
-        k_window_pf<kWinBytes, true, Algo, Sink><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, sink);
-        break;
-      case 31:
-        g_kernel = "k_global<var>";
-        k_global<true, Algo, SinkNt><<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, sink_nt);
-        break;
-      case 23:
-        g_kernel = "k_window2<10224>";
-        k_window2<10224, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
-            b, offsets, obase, n, algo, sink_nt);
-        break;
-      case 24:
-        g_kernel = "k_window2<10224,def>";
-        k_window2<10224, Algo, SinkNt, 0><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
-            b, offsets, obase, n, algo, sink_nt);
-        break;
-      case 25:
-        g_kernel = "k_window2<6144>";
-        k_window2<6144, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
-            b, offsets, obase, n, algo, sink_nt);
-        break;
-      case 11:
-        g_kernel = "k_window<var,nt>";
-        k_window<kWinBytes, true, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, sink_nt);
-        break;
-      default: {
-        // auto: the window that holds a wave's 64 keys at the batch's mean
-        // length (tools/varbench.py, r01): mean <= 160 B (cfg3's 16..256 mix,
-        // mean 136) -> 10224 B at 4 workgroups/CU; longer -> 16 KiB at 2.
-        // Without a byte-count hint (pdht_hip_set_var_bytes_hint) -> 10224.
-        // (k_global<var>, per-lane global reads, measured slower than the
-        // 16 KiB window even at 1-3 KiB keys: varbench r01)
-        if (hint && hint / n > 160) {
-          g_kernel = "k_window<var,nt,16K>";
-          k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(
-              b, offsets, obase, 0, 0, n, algo, sink_nt);
-        } else {
-          g_kernel = "k_window<var,nt,10224>";
-          k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-              b, offsets, obase, 0, 0, n, algo, sink_nt);
-        }
-        break;
-      }
-    }
+    g_kernel = "k_window<var,nt,10224>@4";
+    k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,
+                                                                                    algo, sink_nt);
   }
   HIP_TRY(hipGetLastError());
   return 0;
@@ -462,7 +339,11 @@ static int zero_copy_run(int device, Launch launch) {
   (void)hipSetDevice(prev);
   return rc;
 }
-static bool zero_copy_allowed() { return g_variant.load(std::memory_order_relaxed) != 61; }
+#ifdef PDHT_HIP_TUNING
+static bool zero_copy_allowed() { return tuning_variant() != 61; }  // 61: chunked copies (A/B)
+#else
+static constexpr bool zero_copy_allowed() { return true; }
+#endif
 
 static int slot_reserve(Slot &s, size_t in_bytes, size_t out_bytes) {
   if (!s.st) HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
@@ -538,7 +419,17 @@ static int host_pipeline(int device, Plan plan, Run run) {
   for (size_t c = 0; rc == 0 && plan(c, &k0, &k1); ++c) {
     Slot &s = H.slot[c % kSlots];
     rc = slot_drain(s);
-    if (rc == 0) rc = run(s, k0, k1);
+    if (rc == 0) {
+      rc = run(s, k0, k1);
+      if (rc != 0) {
+        // a chunk that failed half-way may already have queued copies and
+        // harvest entries: let them finish, then forget them, so the slot
+        // never copies into this call's buffers after it has returned
+        if (s.st) (void)hipStreamSynchronize(s.st);
+        s.pending.clear();
+        s.busy = false;
+      }
+    }
     if (rc == 0) {
       hipError_t e = hipEventRecord(s.done, s.st);
       if (e != hipSuccess) rc = fail("%s (hipEventRecord)", hipGetErrorString(e));
@@ -563,8 +454,7 @@ static int host_fixed(const void *keys, size_t keylen, size_t n, size_t out_per_
   const bool pin_in = is_pinned(keys), pin_out = is_pinned(out);
   // Pinned keys and digests: zero-copy.  The kernel itself reads the keys
   // and writes the digests over PCIe, no staging copies: 0.87 vs 0.75
-  // Gkeys/s on 16M x 64 B (62 vs 54 GB/s of PCIe traffic, r01).  Variant 61
-  // keeps the chunked copy pipeline.
+  // Gkeys/s on 16M x 64 B (62 vs 54 GB/s of PCIe traffic, r01).
   void *zk = pin_in && pin_out && zero_copy_allowed() ? pinned_device_ptr(keys) : nullptr;
   void *zo = zk ? pinned_device_ptr(out) : nullptr;
   if (zk && zo)
@@ -596,11 +486,10 @@ using namespace pdht;
 PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.1 (gfx950, CityHash v1.0.x)"; }
 PDHT_API const char *pdht_hip_last_error(void) { return g_err; }
 PDHT_API const char *pdht_hip_last_kernel(void) { return g_kernel; }
-PDHT_API int pdht_hip_set_var_bytes_hint(uint64_t total_bytes) {
-  g_var_bytes_hint = total_bytes;
-  return 0;
-}
+#ifdef PDHT_HIP_TUNING
 PDHT_API int pdht_hip_set_variant(int v) { return g_variant.exchange(v); }
+PDHT_API int pdht_hip_set_blocks_per_cu(int per_cu) { return g_per_cu.exchange(per_cu); }
+#endif
 
 PDHT_API int pdht_hip_device_count(int *count) {
   if (!count) return fail("null count%s", "");
@@ -637,10 +526,10 @@ PDHT_API int pdht_city64_seeds_batch_dev(const void *keys, size_t stride, size_t
   return launch_fixed(keys, stride, keylen, n, AlgoCity64Seeds{seed0, seed1}, Sink64{nullptr, out},
                       ST(s));
 }
-PDHT_API int pdht_city64_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
-                                       uint64_t *out, pdht_hip_stream_t s) {
+PDHT_API int pdht_city64_batch_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                       size_t n, uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
-  return launch_var(bytes, offsets, 0, n, AlgoCity64{}, Sink64{nullptr, out}, ST(s));
+  return launch_var(bytes, nbytes, offsets, 0, n, AlgoCity64{}, Sink64{nullptr, out}, ST(s));
 }
 PDHT_API int pdht_city128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
                                     uint64_t *out, pdht_hip_stream_t s) {
@@ -653,10 +542,10 @@ PDHT_API int pdht_city128_seed_batch_dev(const void *keys, size_t stride, size_t
   if (n && !out) return fail("null out%s", "");
   return launch_fixed(keys, stride, keylen, n, AlgoCity128Seed{lo, hi}, Sink128{nullptr, out}, ST(s));
 }
-PDHT_API int pdht_city128_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
-                                        uint64_t *out, pdht_hip_stream_t s) {
+PDHT_API int pdht_city128_batch_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                        size_t n, uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
-  return launch_var(bytes, offsets, 0, n, AlgoCity128{}, Sink128{nullptr, out}, ST(s));
+  return launch_var(bytes, nbytes, offsets, 0, n, AlgoCity128{}, Sink128{nullptr, out}, ST(s));
 }
 PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
                                        uint64_t *out, pdht_hip_stream_t s) {
@@ -674,11 +563,11 @@ PDHT_API int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride, siz
                         ST(s));
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128Seed{lo, hi}, Sink128{nullptr, out}, ST(s));
 }
-PDHT_API int pdht_citycrc128_batch_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
-                                           uint64_t *out, pdht_hip_stream_t s) {
+PDHT_API int pdht_citycrc128_batch_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                           size_t n, uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
   // any key may exceed 900 B (CityHashCrc256 rounds): CRC-32C tables in LDS
-  return launch_var(bytes, offsets, 0, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
+  return launch_var(bytes, nbytes, offsets, 0, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
 }
 
 PDHT_API int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
@@ -780,8 +669,7 @@ PDHT_API int pdht_city64_batch_var_host(const void *bytes, const uint64_t *offse
     void *zb = pinned_device_ptr(bytes), *zf = pinned_device_ptr(offsets), *zo = pinned_device_ptr(out);
     if (zb && zf && zo)
       return zero_copy_run(device, [&] {
-        g_var_bytes_hint = offsets[n] - offsets[0];
-        return launch_var(zb, static_cast<const u64 *>(zf), 0, n, AlgoCity64{},
+        return launch_var(zb, offsets[n] - offsets[0], static_cast<const u64 *>(zf), 0, n, AlgoCity64{},
                           Sink64{nullptr, static_cast<u64 *>(zo)}, nullptr);
       });
   }
@@ -820,8 +708,7 @@ PDHT_API int pdht_city64_batch_var_host(const void *bytes, const uint64_t *offse
     if (int rc = chunk_in(s, static_cast<const uint8_t *>(bytes) + offsets[a], pin_in, 0, nbytes)) return rc;
     // offsets are always staged (tiny) so that they can be copied as-is
     HIP_TRY(hipMemcpyAsync(s.d_in + off_at, offsets + a, (cnt + 1) * 8, hipMemcpyHostToDevice, s.st));
-    g_var_bytes_hint = nbytes;
-    if (int rc = launch_var(s.d_in, reinterpret_cast<const u64 *>(s.d_in + off_at), offsets[a], cnt,
+    if (int rc = launch_var(s.d_in, nbytes, reinterpret_cast<const u64 *>(s.d_in + off_at), offsets[a], cnt,
                             AlgoCity64{}, Sink64{nullptr, reinterpret_cast<u64 *>(s.d_out)}, s.st))
       return rc;
     return chunk_out(s, out + a, pin_out, 0, cnt * 8);
@@ -911,6 +798,7 @@ PDHT_API int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out,
   if (int rc = current_device(&dev)) return rc;
   Sink64T<true> sink{};
   sink.out = out;
+  g_kernel = "k_fixed_xpose64<fold,nt,d2>@3";
   k_fixed_xpose64<AlgoFold64, Sink64T<true>, true, 2>
       <<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, ST(s)>>>(static_cast<const uint8_t *>(keys), n,
                                                                 AlgoFold64{}, sink);
@@ -921,10 +809,10 @@ PDHT_API int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out,
 // Variable-length counterpart: the default offset-indexed kernel's data
 // movement (window DMA, offsets, LDS reads of every key byte, digest stores)
 // with an XOR fold for the hash.
-PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, const uint64_t *offsets, size_t n,
-                                         uint64_t *out, pdht_hip_stream_t s) {
+PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                         size_t n, uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
-  return launch_var(bytes, offsets, 0, n, AlgoFoldVar{}, Sink64{nullptr, out}, ST(s));
+  return launch_var(bytes, nbytes, offsets, 0, n, AlgoFoldVar{}, Sink64{nullptr, out}, ST(s));
 }
 
 PDHT_API int pdht_hip_splitmix64_fill_dev(uint64_t seed, uint64_t first, size_t nwords,
@@ -953,7 +841,6 @@ PDHT_API int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
 
 // ------------------------------------------------- destination bucketing ---
 namespace pdht {
-static u64 *g_phase = nullptr;  // pdht_hip_set_phase_counters (tuning only)
 struct BucketWs {
   u32 *counts, *chunks;
   u64 *totals, *base;
@@ -994,27 +881,18 @@ struct BucketArgs {
   u64 ntiles;
 };
 
-// SERIAL: one group at a time in the tile-local ranking (variant 41, the r01
-// kernel) instead of the batched LDS atomics (rank_groups).
-template <int L, class Out, bool SERIAL = false, int DBG = 0, int W = kStW, int KPL = kStKPL>
+template <int L, class Out>
 static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
-  static const char *const serial_names[3] = {"k_bucket_scatter_staged<8B,serial-rank>",
-                                              "k_bucket_scatter_staged<16B,serial-rank>",
-                                              "k_bucket_scatter_staged<32B,serial-rank>"};
-  static const char *const wide_names[3] = {"k_bucket_scatter_staged<8B,8x16>", "k_bucket_scatter_staged<16B,8x16>",
-                                            "k_bucket_scatter_staged<32B,8x16>"};
-  g_kernel = (W == 8 ? wide_names : SERIAL ? serial_names : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
-  const size_t bytes = staged_lds_bytes(a.nranks, W, KPL);
-  // the phase-clock build only while pdht_hip_set_phase_counters is active
-  auto fn = g_phase ? &k_bucket_scatter_staged<L, Out, !SERIAL, DBG, true, W, KPL>
-                    : &k_bucket_scatter_staged<L, Out, !SERIAL, DBG, false, W, KPL>;
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = staged_lds_bytes(a.nranks);
+  auto fn = &k_bucket_scatter_staged<L, Out>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
-  const int per_cu = env_int("PDHT_HIP_SCATTER_PER_CU", bytes <= 80 * 1024 ? 2 : 1);  // tuning only
+  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-  fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, g_phase);
+  fn<<<g, kStW * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
   return 0;
 }
 
@@ -1040,7 +918,7 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
   return 0;
 }
 
-enum class BucketKernel { kStaged, kStagedWide, kReg, kGeneric };
+enum class BucketKernel { kStaged, kReg, kGeneric };
 
 // Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
 // (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
@@ -1060,22 +938,21 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   int dev;
   if (int rc = current_device(&dev)) return rc;
   // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter up to
-  // 2048 ranks, register scatter above; other lengths -> generic.  Variants:
-  // 21 forces generic, 22 register, 41 staged with group-serial ranking (r01),
-  // 43 staged with 8 waves x 8192-key tiles, 50-55 timing-only staged builds.
-  const int variant = g_variant.load(std::memory_order_relaxed);
+  // 2048 ranks, register scatter above; other lengths -> generic.
   const uintptr_t al = (uintptr_t)keys | out_al;
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
-  BucketKernel kind = !fixed || variant == 21                   ? BucketKernel::kGeneric
-                      : variant == 22 || nranks > kStagedMaxRanks ? BucketKernel::kReg
-                      : variant == 43                             ? BucketKernel::kStagedWide
-                                                                  : BucketKernel::kStaged;
+  BucketKernel kind = !fixed ? BucketKernel::kGeneric
+                      : nranks > kStagedMaxRanks ? BucketKernel::kReg
+                                                 : BucketKernel::kStaged;
+#ifdef PDHT_HIP_TUNING
+  if (tuning_variant() == 21) kind = BucketKernel::kGeneric;
+  if (tuning_variant() == 22 && fixed) kind = BucketKernel::kReg;
+#endif
   const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
   const int reg_kpl = keysize == 32 ? 8 : 16;
-  const u64 tile = kind == BucketKernel::kStaged       ? kStTile
-                   : kind == BucketKernel::kStagedWide ? (u64)8 * kStKPL * 64
-                   : kind == BucketKernel::kReg        ? (u64)waves * reg_kpl * 64
-                                                       : (u64)waves * kScatKPL * 64;
+  const u64 tile = kind == BucketKernel::kStaged ? kStTile
+                   : kind == BucketKernel::kReg  ? (u64)waves * reg_kpl * 64
+                                                 : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   BucketArgs a{};
@@ -1109,37 +986,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
-    if (kind == BucketKernel::kStagedWide)
-      rc = keysize == 8    ? launch_staged<8, Out, false, 0, 8, kStKPL>(a, out, st, dev)
-           : keysize == 16 ? launch_staged<16, Out, false, 0, 8, kStKPL>(a, out, st, dev)
-                           : launch_staged<32, Out, false, 0, 8, kStKPL>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged && variant == 41)
-      rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
-           : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
-                           : launch_staged<32, Out, true>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged && keysize == 8 && variant >= 50 && variant <= 55)
-      // timing-only builds (wrong results): the r01 kernel with parts removed
-      rc = variant == 50   ? launch_staged<8, Out, true, 1>(a, out, st, dev)
-           : variant == 51 ? launch_staged<8, Out, true, 2>(a, out, st, dev)
-           : variant == 52 ? launch_staged<8, Out, true, 4>(a, out, st, dev)
-           : variant == 53 ? launch_staged<8, Out, true, 8>(a, out, st, dev)
-           : variant == 54 ? launch_staged<8, Out, true, 12>(a, out, st, dev)
-                           : launch_staged<8, Out, true, 15>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged && keysize == 8 && variant == 59) {
-      if constexpr (std::is_same<Out, OutSoA>::value) {  // A/B: non-temporal stores
-        const OutSoAT<true> o2{out.keys, out.mbits, out.ptindex, out.index, out.pt, out.L};
-        rc = launch_staged<8, OutSoAT<true>>(a, o2, st, dev);
-      } else {
-        rc = launch_staged<8, Out>(a, out, st, dev);
-      }
-    } else if (kind == BucketKernel::kStaged && keysize == 8 && variant == 58)
-      rc = launch_staged<8, Out, false, 32>(a, out, st, dev);  // A/B: branch-free stores (correct)
-    else if (kind == BucketKernel::kStaged && keysize == 8 && (variant == 56 || variant == 57))
-      // timing-only: the default kernel with one ballot round (56), and also
-      // without global stores (57)
-      rc = variant == 56 ? launch_staged<8, Out, false, 16>(a, out, st, dev)
-                         : launch_staged<8, Out, false, 28>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged)
+    if (kind == BucketKernel::kStaged)
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
                            : launch_staged<32, Out>(a, out, st, dev);
@@ -1157,11 +1004,6 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
 }
 }  // namespace pdht
 
-PDHT_API int pdht_hip_set_phase_counters(uint64_t *buf) {
-  g_phase = buf;
-  return 0;
-}
-
 PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
   return bucket_layout(nullptr, n, nranks).bytes;
 }
@@ -1169,7 +1011,7 @@ PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
 PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
                                    uint32_t nranks, void *workspace, size_t workspace_bytes,
                                    void *keys_out, uint64_t *mbits_out, uint32_t *ptindex_out,
-                                   uint64_t *index_out, uint64_t *bucket_offsets,
+                                   uint32_t *index_out, uint64_t *bucket_offsets,
                                    pdht_hip_stream_t s) {
   if (int rc = check_place(n, mbits_out, nptes, nranks, nullptr, 0)) return rc;
   const OutSoA out{static_cast<uint8_t *>(keys_out), mbits_out, ptindex_out, index_out, make_fastmod(nptes),

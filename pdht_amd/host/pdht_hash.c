@@ -79,6 +79,9 @@ PDHT_SHIM_API int pdht_hash_batch_dev(pdht_t *dht, const void *keys, size_t n,
                                       void *stream) {
   if (!dht) return PDHT_HIP_ERROR;
   if (dht->hashfn != pdht_hash) return PDHT_HIP_ERROR; /* plugins run on the CPU only */
+#ifdef PDHT_HIP_MPI_FLAVOUR
+  (void)ptindex; /* libmpipdht/hash.c:6-9 computes no ptindex */
+#endif
   return pdht_place_batch_dev(keys, dht->keysize, n,
 #ifndef PDHT_HIP_MPI_FLAVOUR
                               dht->ptl.nptes, (uint32_t)PDHT_HIP_NRANKS(), mbits, ptindex,

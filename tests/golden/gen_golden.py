@@ -14,6 +14,8 @@ the two modulo reductions of hash.c:27 and :29 done in Python.
   python tests/golden/gen_golden.py          # small fixtures (seconds)
   python tests/golden/gen_golden.py --full   # + full-config fold checksums
   python tests/golden/gen_golden.py --extra  # + place/bucket/long folds (added)
+  python tests/golden/gen_golden.py --r02    # + WeakHashLen32WithSeeds(6) vectors
+                                             #   and cfg1 pdht_hash placement folds (added)
 """
 from __future__ import annotations
 
@@ -217,16 +219,71 @@ def folds_extra() -> dict:
     return res
 
 
+def r02_vectors(R) -> dict:
+    """WeakHashLen32WithSeeds6 / WeakHashLen32WithSeeds (city.c:173-198;
+    exported by the reference although city.h does not declare them) on
+    splitmix64 inputs."""
+    R.WeakHashLen32WithSeeds6.restype = O.Uint128
+    R.WeakHashLen32WithSeeds6.argtypes = [C.c_uint64] * 6
+    R.WeakHashLen32WithSeeds.restype = O.Uint128
+    R.WeakHashLen32WithSeeds.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+    nv = 256
+    w6 = O.splitmix64(0xFEEDFACE, 0, nv * 6).reshape(nv, 6)
+    o6 = np.array([u128(R.WeakHashLen32WithSeeds6(*(int(x) for x in row))) for row in w6], np.uint64)
+    b32 = O.splitmix64(0xFEEDFACE, 10_000, nv * 4).view(np.uint8).reshape(nv, 32)
+    sd = O.splitmix64(0xFEEDFACE, 20_000, nv * 2).reshape(nv, 2)
+    o32 = np.array([u128(R.WeakHashLen32WithSeeds(C.c_char_p(b32[i].tobytes()), int(sd[i, 0]), int(sd[i, 1])))
+                    for i in range(nv)], np.uint64)
+    return {"weak6_in": w6, "weak6_out": o6, "weak32_bytes": b32, "weak32_seeds": sd, "weak32_out": o32}
+
+
+CFG1_PLACEMENTS = [(1, 4), (1, 1), (3, 1000), (8, 7)]  # (nptes, nranks): pdht default 1 PTE, 4 ranks
+
+
+def cfg1_folds() -> dict:
+    """cfg1 (BASELINE configs[0]: 1M x 64 B through hash.c -> CityHash64): the
+    reference CityHash64 of every key plus hash.c:27/:29's reductions, for a
+    few (nptes, nranks); folds of mbits, ptindex, rank and the per-rank
+    histogram (putget.c:55's rankputs)."""
+    n, L = M, 64
+    keys = O.fixed_keys(n, L)
+    m = O.apply_ref64(keys, n, L=L, threads=os.cpu_count() or 8)
+    res = {"n": n, "L": L, "mbits": f"{O.fold64(m, 0):016x}", "placements": []}
+    for p, r in CFG1_PLACEMENTS:
+        pt = (m % np.uint64(p)).astype(np.uint64)
+        rk = (m % np.uint64(r)).astype(np.uint64)
+        hist = np.bincount(rk.astype(np.int64), minlength=r).astype(np.uint64)
+        res["placements"].append({"nptes": p, "nranks": r, "ptindex": f"{O.fold64(pt, 0):016x}",
+                                  "rank": f"{O.fold64(rk, 0):016x}", "hist": f"{O.fold64(hist, 0):016x}"})
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true")
     ap.add_argument("--extra", action="store_true",
                     help="add the place/bucket/long folds to config_folds.json")
+    ap.add_argument("--r02", action="store_true",
+                    help="add the WeakHash vectors (npz) and the cfg1 placement folds (json)")
     a = ap.parse_args()
     O.build()
     R = O.ref()
     if R is None:
         sys.exit("oracle/_ref not built: /root/reference is required to regenerate fixtures")
+    if a.r02:
+        npz = os.path.join(HERE, "city_golden.npz")
+        with np.load(npz, allow_pickle=False) as z:
+            vec = {k: z[k] for k in z.files}
+        vec.update(r02_vectors(R))
+        np.savez_compressed(npz, **vec)
+        path = os.path.join(HERE, "config_folds.json")
+        with open(path) as f:
+            doc = json.load(f)
+        doc["configs"]["cfg1_pdht_hash_1M_x64"] = cfg1_folds()
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print("added WeakHash vectors and cfg1 placement folds")
+        return
     if a.extra:
         path = os.path.join(HERE, "config_folds.json")
         with open(path) as f:

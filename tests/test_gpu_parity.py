@@ -55,9 +55,8 @@ def test_generator_matches_oracle(dev, oracle):
     assert (lens.cpu().numpy().astype(np.uint64) == oracle.mixed_lengths(5000)).all()
 
 
-def global_kernel(stride):
-    """k_global's default reader (dword loads; variant 30 = 16-B loads)."""
-    return "k_global<fixed>"
+SMALL_KERNELS = {8: "k_fixed_direct<8,4,nt-store>@8", 16: "k_fixed_direct<16,2,nt>@8",
+                 32: "k_fixed_direct<32,2>@8", 64: "k_fixed_xpose64<nt,d2>@3"}
 
 
 def fixed_kernel(L, stride=None):
@@ -65,8 +64,8 @@ def fixed_kernel(L, stride=None):
     64-key tile (12 KiB or 16 KiB), else per-lane global reads."""
     tile = 63 * (stride or L) + L + 16
     if tile > 16384:
-        return global_kernel(stride or L)
-    return "k_window<fixed,nt,16K>" if tile > 12288 else "k_window<fixed,nt>"
+        return "k_global<fixed>@8"
+    return "k_window<fixed,nt,16K>@2" if tile > 12288 else "k_window<fixed,nt,12K>@3"
 
 
 @pytest.mark.parametrize("L", list(range(0, 300)) + [511, 512, 899, 900, 901, 1000, 2047, 4097])
@@ -76,20 +75,7 @@ def test_city64_every_length(dev, oracle, L):
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
     got = u64(P.city64_batch(to_dev(k, dev)))
     assert (got == oracle.city64_fixed(k)).all()
-    if L in (8, 16, 32, 64):
-        assert P.last_kernel().startswith("k_fixed_"), P.last_kernel()
-    else:
-        assert P.last_kernel() == fixed_kernel(L)
-    if L in (13, 100, 200, 1000):  # the other generic-length kernels too
-        for v, name in ((3, "k_window<fixed>"), (14, "k_window_pf<fixed>"), (11, "k_window<fixed,nt,10224>"),
-                        (27, global_kernel(L)), (28, fixed_kernel(min(L, 255)))):
-            old = P.set_variant(v)
-            try:
-                got = u64(P.city64_batch(to_dev(k, dev)))
-                assert P.last_kernel() == name
-            finally:
-                P.set_variant(old)
-            assert (got == oracle.city64_fixed(k)).all()
+    assert P.last_kernel() == SMALL_KERNELS.get(L, fixed_kernel(L))
 
 
 @pytest.mark.parametrize("L", [0, 1, 3, 8, 13, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 144, 200, 256,
@@ -103,57 +89,26 @@ def test_city128_crc128_lengths(dev, oracle, L):
     assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
 
 
-@pytest.mark.parametrize("L", [256, 901, 1000, 4096])
-def test_long_keys_global_reader(dev, oracle, L):
-    """k_global with and without the 16-B reader (variant 30 asks for it; it
-    applies when every key starts 16-B aligned), aligned and misaligned base."""
-    rng = np.random.default_rng(L + 5)
-    n = 3000
-    flat = to_dev(rng.integers(0, 256, n * L + 16, dtype=np.uint8), dev)
-    for base in (0, 16, 4):
-        kd = flat[base:base + n * L].view(n, L)
-        want = oracle.city64_fixed(kd.cpu().numpy())
-        for v in (0, 30):
-            old = P.set_variant(v)
-            try:
-                got = u64(P.city64_batch(kd))
-                kern = P.last_kernel()
-            finally:
-                P.set_variant(old)
-            assert (got == want).all(), (base, v, kern)
-            if L > 255:
-                a16 = v == 30 and L % 16 == 0 and base % 16 == 0
-                assert kern == ("k_global<fixed,a16>" if a16 else "k_global<fixed>"), kern
-
-
 @pytest.mark.parametrize("L", [256, 272, 320, 1024, 8192])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 5000])
-@pytest.mark.parametrize("variant,kernel", [(32, "k_fixed_chunks")])
-def test_long_keys_chunk_stream(dev, oracle, L, n, variant, kernel):
-    """The long-key CityHash64 variant k_fixed_chunks (32: 64-B chunks of 64
-    keys streamed through LDS): packed and strided rows, ragged tiles, seeded
-    digests and fused placement."""
-    old = P.set_variant(variant)
-    try:
-        _chunk_stream_case(oracle, dev, L, n, kernel)
-    finally:
-        P.set_variant(old)
-
-
-def _chunk_stream_case(oracle, dev, L, n, kernel):
+def test_long_keys(dev, oracle, L, n):
+    """Keys past a 64-key window (k_global): packed and strided rows, ragged
+    tiles, aligned and misaligned bases, seeded digests and fused placement."""
     rng = np.random.default_rng(L * 3 + n)
     for stride in (L, L + 48):
         flat = rng.integers(0, 256, (n, stride), dtype=np.uint8)
         k = flat[:, :L]
         kd = to_dev(flat, dev)[:, :L]
         got = u64(P.city64_batch(kd))
-        assert P.last_kernel() == kernel
-        want = oracle.city64_fixed(np.ascontiguousarray(k))
-        assert (got == want).all(), (L, n, stride)
+        assert P.last_kernel() == "k_global<fixed>@8"
+        assert (got == oracle.city64_fixed(np.ascontiguousarray(k))).all(), (L, n, stride)
+    flat = to_dev(rng.integers(0, 256, n * L + 16, dtype=np.uint8), dev)
+    for base in (4, 1):
+        kd = flat[base:base + n * L].view(n, L)
+        assert (u64(P.city64_batch(kd)) == oracle.city64_fixed(kd.cpu().numpy())).all(), base
     kd = to_dev(np.ascontiguousarray(k), dev)
     s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
     got = u64(P.city64_seeds_batch(kd, s0, s1))
-    assert P.last_kernel() == kernel
     assert [int(x) for x in got[:40]] == [oracle.city64_seeds(r.tobytes(), s0, s1) for r in k[:40]]
     mb, pt, rk = P.place_batch(kd, 7, 1000)
     m2, p2, r2 = oracle.pdht_hash_fixed(np.ascontiguousarray(k), 7, 1000)
@@ -169,7 +124,7 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
     kd = to_dev(k, dev)
     assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
-    assert P.last_kernel() == global_kernel(L)
+    assert P.last_kernel() == "k_global<fixed>@8"
     s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
     got = u64(P.citycrc128_seed_batch(kd[:300], (s0, s1))).reshape(-1, 2)
     assert [tuple(int(x) for x in g) for g in got] == \
@@ -192,30 +147,26 @@ def test_seeded_batches(dev, oracle, L):
     assert [tuple(int(x) for x in g) for g in got] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k]
 
 
-VARIANT_KERNELS = {0: "k_fixed_xpose64", 1: "k_fixed_xpose64<plain>", 2: "k_fixed_lds64",
-                   3: "k_window<fixed>",
-                   4: "k_fixed_lds64<nt-store>", 5: "k_fixed_direct<64,1,nt-load,nt-store>",
-                   6: "k_fixed_direct<64,1>", 7: "k_fixed_xpose64<depth1>",
-                   8: "k_fixed_xpose64<nt-store>", 9: "k_fixed_direct<64,1,nt-store>",
-                   15: "k_fixed_xpose64<depth2>", 26: "k_fixed_xpose64<nt-load,plain-store>"}
+VARIANT_KERNELS = {0: "k_fixed_xpose64<nt,d2>@3", 7: "k_fixed_xpose64<nt,d1>@4",
+                   26: "k_fixed_xpose64<nt-load,plain-store,d2>@3"}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANT_KERNELS))
 def test_64B_kernel_variants_bitexact(dev, oracle, variant):
+    """The product kernel, and the tuning build's alternatives (A/B only)."""
     n = M + 13
     k = oracle.fixed_keys(n, 64)
     want = oracle.city64_fixed(k)
     kd = to_dev(k, dev)
-    old = P.set_variant(variant)
-    try:
+    with P.tuning(variant):
         got = u64(P.city64_batch(kd))
         kern = P.last_kernel()
         got128 = u64(P.citycrc128_batch(kd[:100000]))
-    finally:
-        P.set_variant(old)
     assert kern == VARIANT_KERNELS[variant]
     assert (got == want).all()
     assert (got128 == oracle.city128_fixed(k[:100000], crc=True)).all()
+    assert (u64(P.city64_batch(kd[:1000])) == want[:1000]).all()
+    assert P.last_kernel() == VARIANT_KERNELS[0]  # back on the product library
 
 
 def test_golden_random_64B(dev, golden, oracle):
@@ -236,7 +187,7 @@ def test_edge_layouts(dev, oracle):
     big = rng.integers(0, 256, (1000, 80), dtype=np.uint8)
     bd = to_dev(big, dev)
     got = u64(P.city64_batch(bd[:, :64]))
-    assert P.last_kernel() == fixed_kernel(64, 80)
+    assert P.last_kernel() == fixed_kernel(64, 80) == "k_window<fixed,nt,12K>@3"
     assert (got == oracle.city64_fixed(big[:, :64])).all()
     flat = to_dev(rng.integers(0, 256, 64 * 777 + 1, dtype=np.uint8), dev)
     mis = flat[1:].view(777, 64)
@@ -307,47 +258,47 @@ def test_var_golden_mixed(dev, golden, oracle):
     assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
 
 
-VAR_KERNELS = {0: "auto", 3: "k_window<var>", 10: "k_var_sorted",
-               11: "k_window<var,nt>", 12: "k_window<var,nt,10224>", 13: "k_window<var,nt,16K>",
-               14: "k_window_pf<var>", 23: "k_window2<10224>", 24: "k_window2<10224,def>",
-               25: "k_window2<6144>", 31: "k_global<var>"}
+VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2"}
 
 
 def auto_var_kernel(total_bytes, n):
-    """Variant 0's window choice (launch_var): mean key length > 160 B -> 16 KiB."""
-    return "k_window<var,nt,16K>" if total_bytes // n > 160 else "k_window<var,nt,10224>"
+    """The product's window choice (launch_var): mean key length > 160 B -> 16 KiB."""
+    return "k_window<var,nt,16K>@2" if total_bytes // n > 160 else "k_window<var,nt,10224>@4"
 
 
 @pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
 def test_var_edge_cases(dev, oracle, variant):
-    old = P.set_variant(variant)
-    try:
+    with P.tuning(variant) if variant else _nullctx():
         total, n = _var_edge_cases(dev, oracle)
         want = auto_var_kernel(total, n) if variant == 0 else VAR_KERNELS[variant]
         assert P.last_kernel() == want
-    finally:
-        P.set_variant(old)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 @pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
 def test_var_many_tiles_per_wave(dev, oracle, variant):
-    """Enough keys that every wave of the persistent grid runs several tiles
-    (the double-buffered kernels' steady state), with a few keys longer than
-    any window and empty keys sprinkled in; ragged last tile."""
+    """Enough keys that every wave of the persistent grid runs several tiles,
+    with a few keys longer than any window and empty keys sprinkled in (runs
+    of empty keys fill whole tiles); ragged last tile."""
     rng = np.random.default_rng(23)
     n = 700_001
     lens = rng.integers(0, 300, n)
     lens[rng.integers(0, n, 40)] = 0
+    lens[1000:1200] = 0  # whole tiles of empty keys
     lens[rng.integers(0, n, 12)] = rng.integers(11000, 30000, 12)
     offs = np.zeros(n + 1, np.uint64)
     np.cumsum(lens, out=offs[1:])
     data = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
-    old = P.set_variant(variant)
-    try:
+    with P.tuning(variant) if variant else _nullctx():
         got = u64(P.city64_var_batch(to_dev(data, dev), to_dev(offs.astype(np.int64), dev)))
         kern = P.last_kernel()
-    finally:
-        P.set_variant(old)
     assert variant == 0 or kern == VAR_KERNELS[variant]
     assert (got == oracle.city64_var(data, offs)).all()
 
@@ -377,16 +328,16 @@ def test_var_1M_mixed(dev, oracle):
     data, offs = oracle.mixed_keys(M)
     dd, od = to_dev(data, dev), to_dev(offs.astype(np.int64), dev)
     assert (u64(P.city64_var_batch(dd, od)) == oracle.city64_var(data, offs)).all()
-    assert P.last_kernel() == auto_var_kernel(data.size, M) == "k_window<var,nt,10224>"
-    # the same keys without the byte-count hint (raw C-ABI call): short-key window
+    assert P.last_kernel() == auto_var_kernel(data.size, M) == "k_window<var,nt,10224>@4"
+    # the same keys through the raw C-ABI with nbytes = 0 (unknown): short-key window
     out = torch.empty(M, dtype=torch.int64, device=dev)
-    assert P.lib().pdht_city64_batch_var_dev(dd.data_ptr(), od.data_ptr(), M, out.data_ptr(), None) == 0
-    assert P.last_kernel() == "k_window<var,nt,10224>"
+    assert P.lib().pdht_city64_batch_var_dev(dd.data_ptr(), 0, od.data_ptr(), M, out.data_ptr(), None) == 0
+    assert P.last_kernel() == "k_window<var,nt,10224>@4"
     assert (u64(out) == oracle.city64_var(data, offs)).all()
-    # long keys (mean 192 B): the 16 KiB window
+    # long keys (mean 192 B): the 16 KiB window, chosen from nbytes / n
     data2, offs2 = oracle.mixed_keys(1 << 18, lo=129, hi=256)
     got = u64(P.city64_var_batch(to_dev(data2, dev), to_dev(offs2.astype(np.int64), dev)))
-    assert P.last_kernel() == "k_window<var,nt,16K>"
+    assert P.last_kernel() == "k_window<var,nt,16K>@2"
     assert (got == oracle.city64_var(data2, offs2)).all()
 
 
@@ -411,37 +362,29 @@ def test_place_batch(dev, oracle, L, nptes, nranks):
 
 
 @pytest.mark.parametrize("L", [8, 16, 64])
-@pytest.mark.parametrize("variant", [0, 16, 18, 19, 20])
-def test_place_hist_many_workgroups(dev, oracle, L, variant):
+def test_place_hist_many_workgroups(dev, oracle, L):
     # enough keys for a full persistent grid; hist accumulates across calls
     rng = np.random.default_rng(L + 5)
     k = rng.integers(0, 256, (1 << 21, L), dtype=np.uint8)
     kd = to_dev(k, dev)
     hist = torch.full((1000,), 5, dtype=torch.int64, device=dev)
-    old = P.set_variant(variant)
-    try:
-        P.place_batch(kd, 3, 1000, hist=hist)
-        P.place_batch(kd[:12345], 3, 1000, hist=hist)
-    finally:
-        P.set_variant(old)
+    P.place_batch(kd, 3, 1000, hist=hist)
+    if L in (8, 16):
+        assert P.last_kernel().endswith(",1024>@2")
+    P.place_batch(kd[:12345], 3, 1000, hist=hist)
     _, _, r2 = oracle.pdht_hash_fixed(k, 3, 1000)
     want = 5 + np.bincount(r2, minlength=1000) + np.bincount(r2[:12345], minlength=1000)
     assert (hist.cpu().numpy() == want).all()
 
 
 @pytest.mark.parametrize("L", [8, 16, 32])
-@pytest.mark.parametrize("variant", [0, 16, 17, 18, 19])
-def test_small_key_variants(dev, oracle, L, variant):
-    rng = np.random.default_rng(L + variant)
+def test_small_keys(dev, oracle, L):
+    rng = np.random.default_rng(L)
     k = rng.integers(0, 256, (70001, L), dtype=np.uint8)
     kd = to_dev(k, dev)
-    old = P.set_variant(variant)
-    try:
-        got = u64(P.city64_batch(kd))
-        assert P.last_kernel().startswith(f"k_fixed_direct<{L},")
-        mb, pt, rk = P.place_batch(kd, 7, 1000)
-    finally:
-        P.set_variant(old)
+    got = u64(P.city64_batch(kd))
+    assert P.last_kernel() == SMALL_KERNELS[L]
+    mb, pt, rk = P.place_batch(kd, 7, 1000)
     assert (got == oracle.city64_fixed(k)).all()
     m2, p2, r2 = oracle.pdht_hash_fixed(k, 7, 1000)
     assert (u64(mb) == m2).all()
@@ -449,24 +392,43 @@ def test_small_key_variants(dev, oracle, L, variant):
     assert (rk.cpu().numpy().view(np.uint32) == r2).all()
 
 
+def test_device_wrappers_validate_outputs(dev):
+    """Outputs, histograms and workspaces are checked before any launch: a
+    short histogram, a reused `out` of another size or dtype, or a small
+    workspace raises instead of letting a kernel write past its end."""
+    k = torch.zeros((1000, 8), dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):
+        P.place_batch(k, 3, 1000, hist=torch.zeros(999, dtype=torch.int64, device=dev))
+    with pytest.raises(ValueError):
+        P.place_batch(k, 3, 1000, hist=torch.zeros(1000, dtype=torch.int32, device=dev))
+    mb, pt, rk = P.place_batch(k, 3, 1000)
+    with pytest.raises(ValueError):
+        P.place_batch(k[:999].contiguous(), 3, 1000, out=(mb, pt, rk))
+    with pytest.raises(ValueError):
+        P.city64_batch(k, out=torch.empty(999, dtype=torch.int64, device=dev))
+    out = P.bucket_batch(k, 3, 16)
+    with pytest.raises(ValueError):
+        P.bucket_batch(k, 3, 17, out=out)  # offsets sized for 16 ranks
+    with pytest.raises(ValueError):
+        P.bucket_batch(k, 3, 16, workspace=torch.empty(16, dtype=torch.uint8, device=dev))
+    rec = P.bucket_records(k, 16)
+    with pytest.raises(ValueError):
+        P.bucket_records(k[:500].contiguous(), 16, out=rec)
+    with pytest.raises(ValueError):
+        P.city64_batch(k.cpu())
+    s_other = torch.cuda.Stream(device=dev)
+    assert P.city64_batch(k, stream=s_other).numel() == 1000  # a stream of the right device
+
+
 BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1000, 4096, 4097, 8192)
                 for n in (0, 1, 4095, 100003)]
 BUCKET_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192)
                  for n in (4095, 300007)]
-BUCKET_CASES += [(8, nr, n, v) for v in (58, 59) for nr in (7, 1000, 2048) for n in (1, 4097, 300007)]
-BUCKET_CASES += [(L, nr, n, v) for v in (41, 43) for L in (8, 16, 32) for nr in (1, 7, 1000, 1025, 2048)
-                 for n in (1, 2049, 300007)]
 
 
 def _bucket_kernel(L, nranks, variant):
-    """21 forces the generic-length kernel, 22 the register (unstaged) one,
-    41 the staged one with group-serial ranking, 43 the 8-wave 8192-key staged one."""
-    if variant == 41 and L in (8, 16, 32) and nranks <= 2048:
-        return f"k_bucket_scatter_staged<{L}B,serial-rank>"
-    if variant == 43 and L in (8, 16, 32) and nranks <= 2048:
-        return f"k_bucket_scatter_staged<{L}B,8x16>"
-    if variant in (58, 59) and L == 8 and nranks <= 2048:
-        return "k_bucket_scatter_staged<8B>"
+    """Tuning variants: 21 forces the generic-length kernel, 22 the register
+    (unstaged) one."""
     if variant != 21 and L in (8, 16, 32):
         kind = "reg" if variant == 22 or nranks > 2048 else "staged"
         return f"k_bucket_scatter_{kind}<{L}B>"
@@ -477,17 +439,15 @@ def _bucket_kernel(L, nranks, variant):
 def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     rng = np.random.default_rng(L * 7 + nranks + n)
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
-    old = P.set_variant(variant)
-    try:
+    with P.tuning(variant) if variant else _nullctx():
         ko, mb, pt, ix, offs = P.bucket_batch(to_dev(k, dev), 3, nranks)
         if n:
             assert P.last_kernel() == _bucket_kernel(L, nranks, variant)
-    finally:
-        P.set_variant(old)
     m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, nranks) if n else (
         np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint32))
     order = np.argsort(r2, kind="stable")  # the reference placement, stably bucketed
-    assert (ix.cpu().numpy() == order).all()
+    assert ix.dtype == torch.int32
+    assert (ix.cpu().numpy().view(np.uint32) == order).all()
     assert (u64(mb) == m2[order]).all()
     assert (pt.cpu().numpy().view(np.uint32) == p2[order]).all()
     assert (ko.cpu().numpy() == k[order]).all()
@@ -495,9 +455,29 @@ def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     assert (offs.cpu().numpy() == want_offs).all()
 
 
+@pytest.mark.parametrize("L", [8, 16, 13])
+def test_bucket_optional_outputs(dev, oracle, L):
+    """Each of keys_out / ptindex_out / index_out may be omitted (NULL);
+    mbits and the offsets are the same either way."""
+    rng = np.random.default_rng(L)
+    n = 50_000
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 1, 1000)
+    order = np.argsort(r2, kind="stable")
+    for wk, wp, wi in ((False, False, True), (True, False, False), (False, False, False)):
+        ko, mb, pt, ix, offs = P.bucket_batch(kd, 1, 1000, with_keys=wk, with_ptindex=wp, with_index=wi)
+        assert (ko is not None) == wk and (pt is not None) == wp and (ix is not None) == wi
+        assert (u64(mb) == m2[order]).all()
+        if ix is not None:
+            assert (ix.cpu().numpy().view(np.uint32) == order).all()
+        if ko is not None:
+            assert (ko.cpu().numpy() == k[order]).all()
+
+
 RECORD_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 7, 1000, 2049, 8192)
                 for n in (0, 1, 4095, 100003)]
-RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 41, 43) for L in (8, 16, 32) for nr in (7, 1000, 2048)
+RECORD_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2048)
                  for n in (4097, 300007)]
 
 
@@ -506,11 +486,8 @@ def test_bucket_records(dev, oracle, L, nranks, n, variant):
     """Wire records (message_t header + key) at the bucketed positions."""
     rng = np.random.default_rng(L * 11 + nranks + n)
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
-    old = P.set_variant(variant)
-    try:
+    with P.tuning(variant) if variant else _nullctx():
         rec, offs = P.bucket_records(to_dev(k, dev), nranks, src_rank=5, ht_index=3)
-    finally:
-        P.set_variant(old)
     rb = P.bucket_record_bytes(L)
     assert rb == 24 + (L + 7) // 8 * 8 and tuple(rec.shape) == (n, rb)
     m2, _, r2 = oracle.pdht_hash_fixed(k, 3, nranks) if n else (np.zeros(0, np.uint64), None,
@@ -553,11 +530,8 @@ def test_host_resident_paths(dev, oracle):
     P.city64_batch_host(kp, out=op)  # pinned in and out: zero-copy kernel
     assert (op.numpy().view(np.uint64) == want).all()
     op.zero_()
-    old = P.set_variant(61)  # pinned, through the chunked copy pipeline
-    try:
+    with P.tuning(61):  # pinned, through the chunked copy pipeline (A/B)
         P.city64_batch_host(kp, out=op)
-    finally:
-        P.set_variant(old)
     assert (op.numpy().view(np.uint64) == want).all()
     # zero-copy on pointers inside pinned allocations (offset rows)
     op2 = torch.zeros(n - 7, dtype=torch.int64).pin_memory()
@@ -591,6 +565,27 @@ def test_host_resident_paths(dev, oracle):
     assert (outs[0] == m2).all() and (outs[1] == p2).all() and (outs[2] == r2).all()
 
 
+def test_zero_copy_misaligned_var_keys(dev, oracle):
+    """Pinned variable-length keys at every misaligned base, the last key
+    ending at the last byte of the buffer: the window kernel reads the pinned
+    pages over PCIe, 16-B pieces aligned on ABSOLUTE addresses, so it never
+    reads a block that holds no key byte."""
+    data, offs = oracle.mixed_keys(20000)
+    want = oracle.city64_var(data, offs)
+    buf = torch.zeros(data.size + 64, dtype=torch.uint8).pin_memory().numpy()
+    poffs = torch.zeros(offs.size * 8, dtype=torch.uint8).pin_memory().numpy().view(np.uint64)
+    poffs[:] = offs
+    pout = torch.zeros(want.size * 8, dtype=torch.uint8).pin_memory().numpy().view(np.uint64)
+    for base in (1, 3, 7, 15, 16 + 9):
+        end = buf.size - (base % 16)  # buffers ending at every alignment too
+        start = end - data.size
+        pdata = buf[start:end]
+        pdata[:] = data
+        pout[:] = 0
+        P.city64_var_batch_host(pdata, poffs, out=pout)
+        assert (pout == want).all(), base
+
+
 def test_pdht_hash_batch_default_and_plugin(dev, oracle):
     t = P.PdhtTable(keysize=13, nptes=4, nranks=10)
     k = oracle.fixed_keys(5000, 13)
@@ -606,13 +601,9 @@ def test_pdht_hash_batch_default_and_plugin(dev, oracle):
 def test_cfg2_16M_x64_full_fold(dev, folds):
     f = folds["cfg2_city64_16M_x64"]
     kd = device_keys(f["n"], 64, dev=dev)
-    for variant in (1, 2):
-        old = P.set_variant(variant)
-        try:
-            d = P.city64_batch(kd)
-        finally:
-            P.set_variant(old)
-        assert f"{gpu_fold(d):016x}" == f["total"], variant
+    d = P.city64_batch(kd)
+    assert P.last_kernel() == SMALL_KERNELS[64]
+    assert f"{gpu_fold(d):016x}" == f["total"]
 
 
 def test_cfg4_crc128_16M_full_fold(dev, folds):
@@ -622,7 +613,7 @@ def test_cfg4_crc128_16M_full_fold(dev, folds):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-@pytest.mark.parametrize("variant", [0, 23])
+@pytest.mark.parametrize("variant", [0, 13])
 def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     """8.7 GB of keys: offsets far past 2^31 and 2^32 (64-bit window math)."""
     f = folds["cfg3_city64_64M_mixed"]
@@ -634,21 +625,51 @@ def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     assert total == f["total_bytes"]
     words = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, (total + 7) // 8, device=dev)
     data = words.view(torch.uint8)[:total]
-    old = P.set_variant(variant)
-    try:
+    with P.tuning(variant) if variant else _nullctx():
         d = P.city64_var_batch(data, offs)
-    finally:
-        P.set_variant(old)
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-def test_cfg5_shard0_of_1B(dev, folds):
-    """Shard 0 of the 8-GPU 1B-key config (keys [0, 128M)) on this GPU."""
+def test_cfg5_all_shards_of_1B(dev, folds):
+    """BASELINE configs[4] (1B x 64 B keys over 8 GPUs) on ONE GPU, one shard
+    after another: shard j = keys [j*128M, (j+1)*128M), exactly the slice
+    rank j hashes at N = 8, each checked against the reference's fold of that
+    shard.  Together the 8 shards cover the whole 1B-key stream."""
     f = folds["cfg5_city64_1B_x64"]
     per = f["n"] // 8
-    kd = device_keys(per, 64, dev=dev)
-    d = P.city64_batch(kd)
-    assert f"{gpu_fold(d, 0):016x}" == f["shards"][0]
+    words = torch.empty(per * 8, dtype=torch.int64, device=dev)
+    out = torch.empty(per, dtype=torch.int64, device=dev)
+    total = 0
+    for j in range(8):
+        P.splitmix64_fill(0x5EED5EED5EED5EED, j * per * 8, per * 8, out=words)
+        P.city64_batch(words.view(torch.uint8).view(per, 64), out=out)
+        fj = gpu_fold(out, j * per)
+        assert f"{fj:016x}" == f["shards"][j], j
+        total = (total + fj) & 0xFFFFFFFFFFFFFFFF
+    assert f"{total:016x}" == f["total"]
+
+
+def test_cfg1_place_1M_x64(dev, folds):
+    """BASELINE configs[0] (1M x 64 B keys through hash.c) as a GPU batch:
+    fused placement (mbits, ptindex, rank, rankputs histogram) against the
+    reference folds, for each (nptes, nranks) of the fixture; and the same
+    placement through pdht_hash_batch (host keys, ptl_process_t ranks)."""
+    f = folds["cfg1_pdht_hash_1M_x64"]
+    n = f["n"]
+    kd = device_keys(n, 64, dev=dev)
+    for pl in f["placements"]:
+        hist = torch.zeros(pl["nranks"], dtype=torch.int64, device=dev)
+        mb, pt, rk = P.place_batch(kd, pl["nptes"], pl["nranks"], hist=hist)
+        assert f"{gpu_fold(mb):016x}" == f["mbits"]
+        assert f"{gpu_fold(pt.to(torch.int64) & 0xFFFFFFFF):016x}" == pl["ptindex"]
+        assert f"{gpu_fold(rk.to(torch.int64) & 0xFFFFFFFF):016x}" == pl["rank"]
+        assert f"{gpu_fold(hist):016x}" == pl["hist"]
+    pl = f["placements"][0]
+    t = P.PdhtTable(keysize=64, nptes=pl["nptes"], nranks=pl["nranks"])
+    mb, pt, rk = t.hash_batch(kd.cpu().numpy())
+    from oracle import oracle as O
+    assert f"{O.fold64(mb, 0):016x}" == f["mbits"]
+    assert f"{O.fold64(rk.astype(np.uint64), 0):016x}" == pl["rank"]
 
 
 def test_batches_capture_in_hip_graph(dev, oracle):
@@ -687,4 +708,4 @@ def test_batches_capture_in_hip_graph(dev, oracle):
         m2, p2, r2 = oracle.pdht_hash_fixed(k8h, 3, 1000)
         assert (u64(pl[0]) == m2).all() and (pl[2].cpu().numpy().view(np.uint32) == r2).all()
         order = np.argsort(r2, kind="stable")
-        assert (bk[3].cpu().numpy() == order).all() and (u64(bk[1]) == m2[order]).all()
+        assert (bk[3].cpu().numpy().view(np.uint32) == order).all() and (u64(bk[1]) == m2[order]).all()

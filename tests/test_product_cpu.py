@@ -5,7 +5,12 @@
   bit-exact against the reference golden vectors;
 * pdht_hash / pdht_sethash through the stand-in pdht_t (hash.c:25-41),
   including a user plugin (test/scaling.c:39-43 style identity hash);
-* batch entry points fail loudly (no CPU fallback) when no GPU is usable.
+* batch entry points fail loudly (no CPU fallback) when no GPU is usable;
+* cfg1 (BASELINE configs[0], 1M x 64 B through hash.c -> CityHash64): the
+  product's scalar pdht_hash over the whole config against the reference's
+  golden folds, for both the libpdht and the libmpipdht flavour;
+* the tuning entry points live only in the tuning build;
+* the host wrappers reject bad buffers before C sees them.
 """
 import os
 import re
@@ -34,13 +39,52 @@ def test_library_exports_every_declared_symbol():
     want = set()
     for h in ("pdht_hip.h", "pdht_city.h", "pdht_hash.h"):
         want |= _declared(h)
-    assert len(want) == 44, sorted(want)
+    assert len(want) == 43, sorted(want)
     missing = sorted(want - exported)
     assert not missing, missing
     lib = P.lib()
     for name in want:
         getattr(lib, name)  # resolvable through the loader too
     assert "gfx950" in lib.pdht_hip_version().decode()
+    # the reference city.c's exported symbols, all of them (link-level drop-in)
+    ref = os.path.join(ROOT, "oracle", "_ref", "libcityref.so")
+    if os.path.exists(ref):
+        rsyms = {ln.split()[-1] for ln in subprocess.run(["nm", "-D", "--defined-only", ref],
+                                                          capture_output=True, text=True,
+                                                          check=True).stdout.splitlines()
+                 if " T " in ln}
+        assert rsyms and not (rsyms - exported), sorted(rsyms - exported)
+
+
+def _exports(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+TUNING_SYMS = {"pdht_hip_set_variant", "pdht_hip_set_blocks_per_cu"}
+
+
+def test_tuning_entry_points_only_in_tuning_build():
+    """The product has one kernel per path and no process-global knobs: no
+    variant / per-CU / phase-counter entry points; the tuning build (tools,
+    A/B tests) has them."""
+    prod = _exports(P.LIB_PATH)
+    assert not (TUNING_SYMS & prod)
+    assert not {s for s in prod if "phase" in s or "variant" in s or "hint" in s}
+    assert TUNING_SYMS <= _exports(P.TUNING_LIB_PATH)
+    src = open(os.path.join(ROOT, "pdht_amd", "csrc", "pdht_hip.hip")).read()
+    assert "getenv" not in src
+
+
+def test_weakhash_exports(golden):
+    """WeakHashLen32WithSeeds(6) (city.c:173-198): exported by the reference
+    although city.h omits them; pinned by vectors from the reference."""
+    for row, want in zip(golden["weak6_in"], golden["weak6_out"]):
+        assert P.WeakHashLen32WithSeeds6(*(int(x) for x in row)) == tuple(int(x) for x in want)
+    for b, sd, want in zip(golden["weak32_bytes"], golden["weak32_seeds"], golden["weak32_out"]):
+        assert P.WeakHashLen32WithSeeds(b.tobytes(), int(sd[0]), int(sd[1])) == tuple(int(x) for x in want)
 
 
 def test_scalar_city_api(golden):
@@ -109,6 +153,80 @@ def test_sethash_plugin_scalar_and_batch_on_cpu():
     assert (rk == np.arange(100) % 4).all()
     t.sethash(None)  # back to pdht_hash
     assert t.hash((0).to_bytes(8, "little"))[0] == 0xD7C06285B9DE677A
+
+
+def _cfg1_run(libpath, oracle, folds, nptes, nranks):
+    """The scalar pdht_hash of `libpath` called once per key over cfg1's 1M x
+    64 B keys (C loop: oracle.apply_hashfn drives the function pointer)."""
+    import ctypes as C
+    L = C.CDLL(libpath)
+    L.pdht_hip_table_init.argtypes = [C.c_void_p, C.c_uint, C.c_uint]
+    t = P._PdhtT()
+    L.pdht_hip_table_init(C.byref(t), 64, nptes)
+    C.c_int.in_dll(L, "pdht_hip_shim_nranks").value = nranks
+    f = folds["cfg1_pdht_hash_1M_x64"]
+    keys = oracle.fixed_keys(f["n"], 64)
+    return oracle.apply_hashfn(C.cast(L.pdht_hash, C.c_void_p).value, C.addressof(t), keys), f
+
+
+def test_cfg1_pdht_hash_1M_x64(oracle, folds):
+    """BASELINE configs[0]: 1M x 64 B keys through hash.c -> CityHash64
+    (libpdht/hash.c:25-30), the product's scalar pdht_hash per key, against
+    folds the reference city.c produced (gen_golden.py --r02)."""
+    for pl in folds["cfg1_pdht_hash_1M_x64"]["placements"]:
+        (m, pt, rk), f = _cfg1_run(P.LIB_PATH, oracle, folds, pl["nptes"], pl["nranks"])
+        assert f"{oracle.fold64(m, 0):016x}" == f["mbits"] == folds["cfg1_city64_1M_x64"]["total"]
+        assert f"{oracle.fold64(pt.astype(np.uint64), 0):016x}" == pl["ptindex"]
+        assert f"{oracle.fold64(rk.astype(np.uint64), 0):016x}" == pl["rank"]
+        hist = np.bincount(rk, minlength=pl["nranks"]).astype(np.uint64)
+        assert f"{oracle.fold64(hist, 0):016x}" == pl["hist"]
+
+
+def test_mpi_flavour_pdht_hash(oracle, folds):
+    """libmpipdht/hash.c:6-9: same mbits and rank = mbits % c->size, ptindex
+    left untouched (the library built with -DPDHT_HIP_MPI_FLAVOUR)."""
+    pl = folds["cfg1_pdht_hash_1M_x64"]["placements"][2]
+    (m, pt, rk), f = _cfg1_run(P.MPI_LIB_PATH, oracle, folds, pl["nptes"], pl["nranks"])
+    assert f"{oracle.fold64(m, 0):016x}" == f["mbits"]
+    assert (pt == 0xFFFFFFFF).all()  # never written
+    assert (rk.astype(np.uint64) == m % np.uint64(pl["nranks"])).all()
+    assert f"{oracle.fold64(rk.astype(np.uint64), 0):016x}" == pl["rank"]
+    # and the libpdht flavour does write it
+    (_, pt2, _), _ = _cfg1_run(P.LIB_PATH, oracle, folds, pl["nptes"], pl["nranks"])
+    assert f"{oracle.fold64(pt2.astype(np.uint64), 0):016x}" == pl["ptindex"]
+
+
+def test_host_wrappers_reject_bad_buffers():
+    """Checked before the C call (no GPU needed): wrong dtype, strided views,
+    short outputs and offsets past the data raise ValueError."""
+    k = np.zeros((10, 64), np.uint8)
+    with pytest.raises(ValueError):
+        P.city64_batch_host(k[:, :8])  # strided view
+    with pytest.raises(ValueError):
+        P.city64_batch_host(k.view(np.int8))
+    with pytest.raises(ValueError):
+        P.city64_batch_host(k, out=np.empty(9, np.uint64))
+    with pytest.raises(ValueError):
+        P.city64_batch_host(k, out=np.empty(10, np.int32))
+    with pytest.raises(ValueError):
+        P.citycrc128_batch_host(k, out=np.empty(19, np.uint64))
+    with pytest.raises(ValueError):
+        P.place_batch_host(k[:, :8].copy(), 3, 4, out=(np.empty(10, np.uint64), np.empty(9, np.uint32),
+                                                       np.empty(10, np.uint32)))
+    data = np.zeros(100, np.uint8)
+    with pytest.raises(ValueError):
+        P.city64_var_batch_host(data, np.array([0, 50, 101], np.uint64))
+    with pytest.raises(ValueError):
+        P.city64_var_batch_host(data, np.array([0, 50, 100], np.uint64), out=np.empty(1, np.uint64))
+    import torch
+    with pytest.raises(ValueError):
+        P.city64_batch_host(torch.zeros((10, 64), dtype=torch.uint8)[:, :32])
+
+
+def test_device_wrappers_reject_cpu_tensors():
+    import torch
+    with pytest.raises(ValueError):
+        P.city64_batch(torch.zeros((4, 64), dtype=torch.uint8))
 
 
 def test_batch_fails_loudly_without_gpu():

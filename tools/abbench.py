@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of kernel variants (tuning build, libpdht_hip_tuning.so):
+one process, rounds interleaved across variants, HIP events on the launch
+stream; every variant's output is compared with the product kernel's.
+
+  python tools/abbench.py --work cfg2 --variants 0,7,26 [--per-cu 0,2,3,4]
+  works: cfg2 (16M x 64 B City64), cfg4 (Crc128), cfg3 (64M mixed 16..256 B),
+         long (1M x 1 KiB Crc128), long64 (1M x 1 KiB City64),
+         place (16M x 8 B, nptes 3, nranks 1024, histogram),
+         bucket (16M x 8 B, 1024 ranks, keys+mbits+ptindex+index)
+Variant 0 runs through the PRODUCT library; the others through the tuning
+build (pdht_amd.tuning).  Numbers: median / min ms and algorithmic GB/s.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import pdht_amd as P  # noqa: E402
+
+SEED = 0x5EED5EED5EED5EED
+M = 1 << 20
+
+
+def workload(name, dev):
+    """(step(), result-for-equality(), algorithmic bytes per step)"""
+    if name in ("cfg2", "cfg4", "long", "long64", "place", "bucket"):
+        L = {"cfg2": 64, "cfg4": 64, "long": 1024, "long64": 1024, "place": 8, "bucket": 8}[name]
+        n = M if name in ("long", "long64") else 16 * M
+        keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
+        if name in ("cfg2", "long64"):
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            return (lambda: P.city64_batch(keys, out=out)), (lambda: out.clone()), n * (L + 8)
+        if name in ("cfg4", "long"):
+            out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+            return (lambda: P.citycrc128_batch(keys, out=out)), (lambda: out.clone()), n * (L + 16)
+        if name == "place":
+            hist = torch.zeros(1024, dtype=torch.int64, device=dev)
+            outs = P.place_batch(keys, 3, 1024)
+            return ((lambda: P.place_batch(keys, 3, 1024, hist=hist, out=outs)),
+                    (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 24)
+        ws = torch.empty(P.bucket_workspace_bytes(n, 1024), dtype=torch.uint8, device=dev)
+        outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
+        return ((lambda: P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)),
+                (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (8 + 8 + 8 + 4 + 4))
+    n = 64 * M
+    lens = P.mixed_lengths(0x1E575EED1E575EED, 0, n, 16, 256, device=dev)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item())
+    data = P.splitmix64_fill(SEED, 0, (total + 7) // 8, device=dev).view(torch.uint8)[:total]
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    return (lambda: P.city64_var_batch(data, offs, out=out)), (lambda: out.clone()), total + 16 * n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--work", default="cfg2")
+    ap.add_argument("--variants", default="0")
+    ap.add_argument("--per-cu", default="0")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    step, result, nbytes = workload(a.work, dev)
+    combos = [(int(v), int(pc)) for v in a.variants.split(",") for pc in a.per_cu.split(",")]
+
+    class Ctx:
+        def __init__(self, v, pc):
+            self.c = P.tuning(v, pc) if (v or pc) else None
+
+        def __enter__(self):
+            if self.c:
+                self.c.__enter__()
+
+        def __exit__(self, *e):
+            if self.c:
+                self.c.__exit__(*e)
+
+    ref, stats = None, {}
+    for v, pc in combos:
+        with Ctx(v, pc):
+            step()
+            torch.cuda.synchronize()
+            r = result()
+            if ref is None:
+                ref = r
+            stats[(v, pc)] = {"ok": bool(torch.equal(r, ref)), "kernel": P.last_kernel(), "ms": []}
+    for _ in range(a.rounds):
+        for v, pc in combos:
+            with Ctx(v, pc):
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(a.reps)]
+                for s, e in ev:
+                    s.record()
+                    step()
+                    e.record()
+                torch.cuda.synchronize()
+                stats[(v, pc)]["ms"].extend(s.elapsed_time(e) for s, e in ev)
+    rows = []
+    for (v, pc), t in stats.items():
+        med = float(np.median(t["ms"]))
+        rows.append({"work": a.work, "variant": v, "per_cu": pc, "kernel": t["kernel"], "ok": t["ok"],
+                     "median_ms": round(med, 4), "min_ms": round(float(np.min(t["ms"])), 4),
+                     "GBps": round(nbytes / med / 1e6, 1), "frac_8TBps": round(nbytes / med / 1e6 / 8000, 4)})
+    for r in sorted(rows, key=lambda r: r["median_ms"]):
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
