@@ -333,8 +333,8 @@ def main():
         "parity": parity,
     }
     if world > 1:
-        res["per_rank"] = per_rank_report(torch, D, dev, rank, local, world, n, bytes_per_key, kern_ms,
-                                          elapsed, a.steps, P)
+        res["per_rank"] = D.per_rank_report(rank, local, world, n, bytes_per_key, kern_ms, elapsed, a.steps,
+                                            PEAK_HBM_GBPS, device=dev)
     if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:
         hr = host_rate(P, torch, n, cfg, D, dev)
         if rank == 0:
@@ -345,30 +345,6 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def per_rank_report(torch, D, dev, rank, local, world, n, bytes_per_key, kern_ms, elapsed, steps, P):
-    """Every rank's own numbers (gathered): device, kernel time, Gkeys/s and
-    roofline fraction per GPU, and the RCCL world (per-GPU and
-    aggregate at 1/2/4/8 GPUs)."""
-    import socket
-
-    import torch.distributed as dist
-    props = torch.cuda.get_device_properties(dev)
-    mine = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": dev.index,
-            "name": props.name, "pci": f"{getattr(props, 'pci_domain_id', 0):04x}:"
-                                       f"{getattr(props, 'pci_bus_id', 0):02x}:"
-                                       f"{getattr(props, 'pci_device_id', 0):02x}",
-            "kernel_ms": round(kern_ms, 4),
-            "Gkeys_s": round(n / (kern_ms / 1e3) / 1e9, 3),
-            "frac": round(bytes_per_key * n / (kern_ms / 1e3) / 1e9 / PEAK_HBM_GBPS, 4),
-            "wall_Gkeys_s": round(n * steps / elapsed / 1e9, 3)}
-    allr = [None] * world
-    dist.all_gather_object(allr, mine)
-    return {"world_size": world, "backend": dist.get_backend(),
-            "ranks": allr,
-            "Gkeys_s": [r["Gkeys_s"] for r in allr], "frac": [r["frac"] for r in allr],
-            "aggregate_kernel_Gkeys_s": round(sum(r["Gkeys_s"] for r in allr), 3)}
 
 
 def load_traffic(cfg, n, kernel):

@@ -225,6 +225,39 @@ __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW wo
   return off + x - v;
 }
 
+// Per-wave bucket run tables of the staged scatter: u32 counters, or (PACK)
+// two u16 counters per u32 word -- a 4096-key tile never counts past 4096 in
+// one bucket, so the low half never carries into the high one -- which
+// halves the table's LDS (16 -> 8 KiB at 1024 ranks).  Wave w's counters
+// start at w * stride (stride = nranks, rounded up to even when packed so a
+// word never straddles two waves).
+template <bool PACK>
+struct RunTab {
+  u32 *t;
+  u32 stride;
+  __device__ __forceinline__ u32 words(u32 W) const { return PACK ? W * stride / 2 : W * stride; }
+  __device__ __forceinline__ u32 get(u32 w, u32 r) const {
+    const u32 i = w * stride + r;
+    return PACK ? (t[i >> 1] >> (16 * (i & 1))) & 0xffffu : t[i];
+  }
+  // only the thread owning rank pair (r & ~1, r | 1) of every wave writes it
+  __device__ __forceinline__ void set(u32 w, u32 r, u32 v) const {
+    const u32 i = w * stride + r;
+    if constexpr (PACK) {
+      const u32 sh = 16 * (i & 1);
+      t[i >> 1] = (t[i >> 1] & ~(0xffffu << sh)) | (v << sh);
+    } else {
+      t[i] = v;
+    }
+  }
+  // returns the counter's old value
+  __device__ __forceinline__ u32 add(u32 w, u32 r, u32 v) const {
+    const u32 i = w * stride + r;
+    if constexpr (PACK) return (atomicAdd(&t[i >> 1], v << (16 * (i & 1))) >> (16 * (i & 1))) & 0xffffu;
+    else return atomicAdd(&t[i], v);
+  }
+};
+
 // Stable tile-local slots of a wave's KPL groups of 64 keys.  Lanes with the
 // same bucket find each other by ballots; each group's leader (its lowest
 // lane) claims the bucket's next run of slots with one returning LDS atomic on
@@ -233,8 +266,8 @@ __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW wo
 // groups before it) and a single wait precedes the shuffles that hand every
 // lane its leader's base: two LDS round trips per tile instead of two per
 // group (the r01 form).
-template <int KPL>
-__device__ __forceinline__ void rank_groups(u32 *myrun, const u32 (&rr)[KPL], u32 q0, u32 tn,
+template <int KPL, class Tab>
+__device__ __forceinline__ void rank_groups(const Tab &run, u32 wave, const u32 (&rr)[KPL], u32 q0, u32 tn,
                                             u32 nbits, u32 (&lp)[KPL]) {
   const u32 lane = threadIdx.x & 63;
   const u64 below = (1ull << lane) - 1;
@@ -246,7 +279,7 @@ __device__ __forceinline__ void rank_groups(u32 *myrun, const u32 (&rr)[KPL], u3
     const u32 ahead = (u32)__builtin_popcountll(same & below);
     al[g] = ahead | ((same ? (u32)__builtin_ctzll(same) : 0u) << 8);
     base[g] = 0;
-    if (valid && ahead == 0) base[g] = atomicAdd(&myrun[rr[g]], (u32)__builtin_popcountll(same));
+    if (valid && ahead == 0) base[g] = run.add(wave, rr[g], (u32)__builtin_popcountll(same));
   }
 #pragma unroll
   for (int g = 0; g < KPL; ++g) lp[g] = (u32)__shfl((int)base[g], (int)(al[g] >> 8)) + (al[g] & 0xffu);
@@ -363,34 +396,38 @@ struct OutRec {
 // 8-B keys, 1024 ranks.
 constexpr int kStW = 4, kStKPL = 16;
 constexpr u32 kStTile = kStW * kStKPL * 64;
-constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL) {
-  return (size_t)W * KPL * 64 * 10 + (size_t)W * nranks * 4 + (size_t)nranks * 4;
+constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL, bool PACK = false) {
+  return (size_t)W * KPL * 64 * 10 + (PACK ? (size_t)W * ((nranks + 1) & ~1u) * 2 : (size_t)W * nranks * 4) +
+         (size_t)nranks * 4;
 }
 // Per-entry branches around the stores measured 12 % faster than clamped
 // branch-free stores (r01), although the branch-free form has no SGPR spills:
 // the compiler then batches each array's stores, and the store order changes
 // how the runs meet in L2.
-template <int L, class Out, int W = kStW, int KPL = kStKPL>
-__global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_scatter_staged(
+template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(PACK ? 3 : (L == 8 || W == 8) ? 2 : 1)))
+void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, u32 nbits, TileStarts ts, u64 ntiles,
     Out out) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                              // [kTile]
   uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile]
-  u32 *run = reinterpret_cast<u32 *>(sidx + kTile);              // [W][nranks]
-  u32 *delta = run + W * nranks;                                // [nranks]
+  const RunTab<PACK> run{reinterpret_cast<u32 *>(sidx + kTile), PACK ? (nranks + 1) & ~1u : nranks};
+  u32 *delta = run.t + run.words(W);                            // [nranks]
   __shared__ u32 scan_scratch[W];
   constexpr u32 kSub = KPL * 64;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  u32 *myrun = run + wave * nranks;
-  const u32 per = (nranks + kB - 1) / kB;
+  // each thread owns a run of ranks for the scan (an even run when packed:
+  // a word's two counters then have one owner)
+  u32 per = (nranks + kB - 1) / kB;
+  if (PACK) per = (per + 1) & ~1u;
   const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
   for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kTile;
     const u32 tn = (u32)min((u64)kTile, n - tbase);
-    for (u32 j = threadIdx.x; j < W * nranks; j += kB) run[j] = 0;
+    for (u32 j = threadIdx.x; j < run.words(W); j += kB) run.t[j] = 0;
     const u32 q0 = wave * kSub + lane;
     RegReader<L / 4> kr[KPL];
 #pragma unroll
@@ -405,25 +442,25 @@ __global__ __launch_bounds__(W * 64, (L == 8 || W == 8) ? 2 : 1) void k_bucket_s
     __syncthreads();
 #pragma unroll
     for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) atomicAdd(&myrun[rr[g]], 1u);
+      if (q0 + g * 64 < tn) run.add(wave, rr[g], 1u);
     __syncthreads();
     u32 s = 0;
     for (u32 r = rb0; r < rb1; ++r)
 #pragma unroll
-      for (int w = 0; w < W; ++w) s += run[w * nranks + r];
+      for (int w = 0; w < W; ++w) s += run.get(w, r);
     u32 acc = block_exclusive_scan<W>(s, scan_scratch);
     for (u32 r = rb0; r < rb1; ++r) {
       delta[r] = ts.at(r, t) - acc;
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const u32 v = run[w * nranks + r];
-        run[w * nranks + r] = acc;
+        const u32 v = run.get(w, r);
+        run.set(w, r, acc);
         acc += v;
       }
     }
     __syncthreads();
     u32 lp[KPL];
-    rank_groups<KPL>(myrun, rr, q0, tn, nbits, lp);
+    rank_groups<KPL>(run, wave, rr, q0, tn, nbits, lp);
 #pragma unroll
     for (int g = 0; g < KPL; ++g)
       if (q0 + g * 64 < tn) {

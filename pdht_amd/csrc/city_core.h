@@ -394,66 +394,110 @@ constexpr Crc32cTables make_crc32c_tables() {
 __device__ __constant__ const Crc32cTables kCrcDev = make_crc32c_tables();
 static constexpr Crc32cTables kCrcHost = make_crc32c_tables();
 
-// Where the tables live: CrcConstTab = the compile-time tables (host; device
-// constant memory), kernels.h adds an LDS copy for the GPU's long-key path.
+// Slicing-by-8 over the compile-time tables: one lookup per byte.
+PDHT_HD u32 crc32c_slice8(const Crc32cTables &T, u64 x) {
+  return T.t[7][x & 0xff] ^ T.t[6][(x >> 8) & 0xff] ^ T.t[5][(x >> 16) & 0xff] ^ T.t[4][(x >> 24) & 0xff] ^
+         T.t[3][(x >> 32) & 0xff] ^ T.t[2][(x >> 40) & 0xff] ^ T.t[1][(x >> 48) & 0xff] ^ T.t[0][x >> 56];
+}
+
+// The same map in 5-bit slices: CRC-32C of a 64-bit word with a zero initial
+// CRC is GF(2)-linear in the word, so it is the XOR of the contributions of
+// its 13 five-bit fields (12 x 5 bits + the top 4), each a 32-entry table:
+// T5[k][f] = crc(f << 5k).  13 lookups instead of 8, but a 32-entry table
+// spans 32 distinct LDS banks, so 64 lanes reading one table at random
+// indices never conflict (identical indices broadcast); slicing-by-8's
+// 256-entry tables conflicted 4.3x (profiles/r01/sq_long).
+struct Crc32c5Tables {
+  u32 t[13][32];
+};
+constexpr Crc32c5Tables make_crc32c5_tables() {
+  Crc32c5Tables F{};
+  const Crc32cTables S = make_crc32c_tables();
+  for (u32 k = 0; k < 13; ++k)
+    for (u32 f = 0; f < 32; ++f) {
+      const u64 x = k < 12 || f < 16 ? (u64)f << (5 * k) : 0;
+      F.t[k][f] = S.t[7][x & 0xff] ^ S.t[6][(x >> 8) & 0xff] ^ S.t[5][(x >> 16) & 0xff] ^
+                  S.t[4][(x >> 24) & 0xff] ^ S.t[3][(x >> 32) & 0xff] ^ S.t[2][(x >> 40) & 0xff] ^
+                  S.t[1][(x >> 48) & 0xff] ^ S.t[0][x >> 56];
+    }
+  return F;
+}
+__device__ __constant__ const Crc32c5Tables kCrc5Dev = make_crc32c5_tables();
+
+// Where the tables live: CrcConstTab = the compile-time slicing-by-8 tables
+// (host; device constant memory); kernels.h adds the LDS copy of the 5-bit
+// tables for the GPU's long-key path.
 struct CrcConstTab {
-  PDHT_HD u32 operator()(u32 slice, u32 byte) const {
+  PDHT_HD u32 crc64(u64 x) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return kCrcDev.t[slice][byte];
+    return crc32c_slice8(kCrcDev, x);
 #else
-    return kCrcHost.t[slice][byte];
+    return crc32c_slice8(kCrcHost, x);
 #endif
   }
 };
 
 template <class Tab = CrcConstTab>
 PDHT_HD u64 crc32c_u64(u64 crc, u64 v, const Tab &T = Tab{}) {
-  const u64 x = v ^ (u32)crc;
-  return T(7, x & 0xff) ^ T(6, (x >> 8) & 0xff) ^ T(5, (x >> 16) & 0xff) ^ T(4, (x >> 24) & 0xff) ^
-         T(3, (x >> 32) & 0xff) ^ T(2, (x >> 40) & 0xff) ^ T(1, (x >> 48) & 0xff) ^ T(0, (u32)(x >> 56));
+  return T.crc64(v ^ (u32)crc);
 }
 
-// city.c:407-473 (CityHashCrc256Long), len >= 240
+// city.c:407-473 (CityHashCrc256Long), len >= 240.  Each 240-byte block is
+// fetched as ONE span (60 dwords; dwordx4 loads for 16-B aligned keys) and
+// its six 40-byte CHUNKs work on compile-time offsets into it: one memory
+// round trip per block instead of one per chunk (the long-key kernels read
+// each lane's key straight from global memory, and waited on every chunk).
 template <class R, class Tab = CrcConstTab>
 PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T = Tab{}) {
-  u64 a = fetch64(s, 56) + kK0;
-  u64 b = fetch64(s, 96) + kK0;
+  Words<60> q = s.template span<240>(0);  // block 0 (len >= 240)
+  u64 a = q.w64(56) + kK0;
+  u64 b = q.w64(96) + kK0;
   u64 c = out[0] = mix16(b, len);
-  u64 d = out[1] = fetch64(s, 120) * kK0 + len;
-  u64 e = fetch64(s, 184) + seed;
+  u64 d = out[1] = q.w64(120) * kK0 + len;
+  u64 e = q.w64(184) + seed;
   u64 f = seed, g = 0, h = 0, i = 0, j = 0;
   u64 t = c + d;
   u32 o = 0;
-  auto chunk = [&](u64 mult, u32 flip) {  // one 40-byte CHUNK (city.c:425-440)
-    const Words<10> q = s.template span<40>(o);
+  // one 40-byte CHUNK (city.c:425-440) over the words w0..w4
+  auto chunk = [&](u64 w0, u64 w1, u64 w2, u64 w3, u64 w4, u64 mult, u32 flip) {
     const u64 a0 = a;
-    a = rotr(b, 41u ^ flip) * mult + q.w64(0);
-    b = rotr(c, 27u ^ flip) * mult + q.w64(8);
-    c = rotr(d, 41u ^ flip) * mult + q.w64(16);
-    d = rotr(e, 33u ^ flip) * mult + q.w64(24);
-    e = rotr(t, 25u ^ flip) * mult + q.w64(32);
+    a = rotr(b, 41u ^ flip) * mult + w0;
+    b = rotr(c, 27u ^ flip) * mult + w1;
+    c = rotr(d, 41u ^ flip) * mult + w2;
+    d = rotr(e, 33u ^ flip) * mult + w3;
+    e = rotr(t, 25u ^ flip) * mult + w4;
     t = a0;
     f = crc32c_u64(f, a, T);
     g = crc32c_u64(g, b, T);
     h = crc32c_u64(h, c, T);
     i = crc32c_u64(i, d, T);
     j = crc32c_u64(j, e, T);
+  };
+  auto chunk_at = [&](const Words<60> &w, u32 base, u64 mult, u32 flip) {
+    chunk(w.w64(base), w.w64(base + 8), w.w64(base + 16), w.w64(base + 24), w.w64(base + 32), mult, flip);
+  };
+  auto chunk_span = [&](u64 mult, u32 flip) {
+    const Words<10> w = s.template span<40>(o);
+    chunk(w.w64(0), w.w64(8), w.w64(16), w.w64(24), w.w64(32), mult, flip);
     o += 40;
   };
   const u64 blocks = len / 240;
   u64 rest = len - blocks * 240;
   for (u64 k = 0; k < blocks; ++k) {
-    chunk(1, 1);
-    chunk(kK0, 0);
-    chunk(1, 1);
-    chunk(kK0, 0);
-    chunk(1, 1);
-    chunk(kK0, 0);
+    // (prefetching the next block as well measured equal, r02: 165 VGPRs)
+    if (k) q = s.template span<240>(o);
+    chunk_at(q, 0, 1, 1);
+    chunk_at(q, 40, kK0, 0);
+    chunk_at(q, 80, 1, 1);
+    chunk_at(q, 120, kK0, 0);
+    chunk_at(q, 160, 1, 1);
+    chunk_at(q, 200, kK0, 0);
+    o += 240;
   }
-  for (; rest >= 40; rest -= 40) chunk(kK0, 0);
+  for (; rest >= 40; rest -= 40) chunk_span(kK0, 0);
   if (rest > 0) {
     o = o + (u32)rest - 40;
-    chunk(kK0, 0);
+    chunk_span(kK0, 0);
   }
   j += i << 32;
   a = mix16(a, j);

@@ -68,11 +68,31 @@ struct LdsReader {
 // it, i.e. wait for the next tile's prefetch on the common path too.
 typedef const __attribute__((address_space(1))) u32 gu32;
 typedef const __attribute__((address_space(1))) uint8_t gu8;
-struct GlobalReader {
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+// A16: every key starts 16-B aligned (fixed keys, aligned base and stride):
+// spans at 16-B aligned offsets load as dwordx4, a quarter of the
+// instructions (the CRC-256 rounds read 240-B blocks at multiples of 240).
+template <bool A16 = false>
+struct GlobalReaderT {
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
+    if constexpr (A16 && N % 16 == 0) {
+      if ((a & 15) == 0) {
+        gu32x4 *q = reinterpret_cast<gu32x4 *>(a);
+        Words<N / 4> w;
+#pragma unroll
+        for (int j = 0; j < N / 16; ++j) {
+          const u32x4 v = q[j];
+          w.d[4 * j + 0] = v.x;
+          w.d[4 * j + 1] = v.y;
+          w.d[4 * j + 2] = v.z;
+          w.d[4 * j + 3] = v.w;
+        }
+        return w;
+      }
+    }
     gu32 *q = reinterpret_cast<gu32 *>(a & ~(uintptr_t)3);
     const u32 r = (u32)(a & 3);
     u32 raw[N / 4 + 1];
@@ -89,6 +109,7 @@ struct GlobalReader {
     return reinterpret_cast<gu8 *>(reinterpret_cast<uintptr_t>(p))[o];
   }
 };
+typedef GlobalReaderT<false> GlobalReader;
 
 // ------------------------------------------------------------ algorithms ---
 struct AlgoCity64 {
@@ -131,13 +152,23 @@ struct AlgoCrc128Seed {
   }
 };
 
-// CRC-32C slicing tables in LDS (8 KiB per workgroup) for batches that may
-// hold keys > 900 B (CityHashCrc256 path, city.c:407-517): one lookup per key
-// byte, 64 lanes at random table words.  From constant memory those lookups
-// are per-lane vector loads through the TA, 4x slower (tools/longbench.py).
+// CRC-32C tables in LDS for batches that may hold keys > 900 B
+// (CityHashCrc256 path, city.c:407-517): the 5-bit-slice tables of
+// city_core.h, 13 x 32 entries = 1664 B per workgroup, every lookup
+// conflict-free.  (r01 kept the slicing-by-8 tables here, 8 KiB: one lookup
+// per byte but 4.3x bank conflicts; from constant memory those lookups are
+// per-lane vector loads through the TA, 4x slower again.)
 struct CrcLdsTab {
-  const u32 *t;
-  __device__ __forceinline__ u32 operator()(u32 slice, u32 byte) const { return t[slice * 256 + byte]; }
+  const u32 *t;  // [13][32]
+  __device__ __forceinline__ u32 crc64(u64 x) const {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    u32 r = t[0 * 32 + (lo & 31)] ^ t[1 * 32 + ((lo >> 5) & 31)] ^ t[2 * 32 + ((lo >> 10) & 31)] ^
+            t[3 * 32 + ((lo >> 15) & 31)] ^ t[4 * 32 + ((lo >> 20) & 31)] ^ t[5 * 32 + ((lo >> 25) & 31)];
+    r ^= t[6 * 32 + (__builtin_amdgcn_alignbit(hi, lo, 30) & 31)];
+    r ^= t[7 * 32 + ((hi >> 3) & 31)] ^ t[8 * 32 + ((hi >> 8) & 31)] ^ t[9 * 32 + ((hi >> 13) & 31)] ^
+         t[10 * 32 + ((hi >> 18) & 31)] ^ t[11 * 32 + ((hi >> 23) & 31)] ^ t[12 * 32 + (hi >> 28)];
+    return r;
+  }
 };
 template <class Base>
 struct CrcLds : Base {
@@ -170,8 +201,8 @@ struct HasCrcLds<A, decltype((void)A::kCrcLds)> {
 template <class Algo>
 __device__ __forceinline__ void algo_init(Algo &a) {
   if constexpr (HasCrcLds<Algo>::value) {
-    __shared__ u32 tab[8 * 256];
-    for (u32 k = threadIdx.x; k < 8 * 256; k += blockDim.x) tab[k] = kCrcDev.t[k >> 8][k & 255];
+    __shared__ u32 tab[13 * 32];
+    for (u32 k = threadIdx.x; k < 13 * 32; k += blockDim.x) tab[k] = kCrc5Dev.t[k >> 5][k & 31];
     __syncthreads();
     a.tab = tab;
   }
@@ -211,6 +242,19 @@ struct AlgoFoldVar {
     return ((u64)b << 32) | a;
   }
 };
+
+#ifdef PDHT_HIP_TUNING
+// Tuning-only calibrations of the variable-length window kernel: the digest
+// is the key length (no key byte is read from LDS), so the kernel is its
+// window DMA, offsets loads and digest stores alone.
+struct AlgoLenOnly {
+  typedef u64 Out;
+  template <class R>
+  __device__ __forceinline__ Out operator()(const R &, u64 len) const {
+    return len;
+  }
+};
+#endif
 
 // ----------------------------------------------------------------- sinks ---
 // Where a digest goes.  init()/flush() run once per workgroup around the
@@ -468,7 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restr
 // Any key length.  VAR: key i = bytes[offsets[i]-obase, offsets[i+1]-obase);
 // otherwise key i = bytes[i*stride, i*stride+keylen).  WIN = LDS bytes per
 // wave.  AUX = cache-policy bits of the LDS-DMA (2 = non-temporal).
-template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0>
+template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0, int ALIGN = 16>
 __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -519,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
       first = offsets[k0] - obase;
     else
       first = k0 * stride;
-    const u64 wlo = (base + first) & ~(u64)15;
+    const u64 wlo = (base + first) & ~(u64)(ALIGN - 1);
     const u64 span = whi > first ? base + whi - wlo : 0;  // a tile of empty keys reads nothing
     const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
     // DMA the window: piece j moves 1 KiB, lane l's 16 B to LDS 1024j+16l.
@@ -549,12 +593,207 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
   sink.flush();
 }
 
+// ------------------------------------- window kernel, offsets prefetched ---
+// Offset-indexed keys, as k_window<WIN, true>, with the next tile's offsets
+// loaded while this tile's window streams in: the window DMA of tile t+1 is
+// issued as soon as tile t is hashed, instead of after another round trip
+// for its offsets (k_window: offsets -> DMA -> hash, two dependent memory
+// latencies per tile).  One vector load per tile and lane (offsets[k0+lane];
+// a key's end is its right neighbour's start) plus one uniform load of
+// offsets[kend].
+template <int WIN, class Algo, class Sink, int AUX = 2>
+__global__ __launch_bounds__(kBlock) void k_window_var(const uint8_t *__restrict__ bytes,
+                                                       const u64 *__restrict__ offsets, u64 obase, u64 n,
+                                                       Algo algo, Sink sink) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  algo_init(algo);
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *lds = win_all + wave * (WIN / 4);
+  const u64 base = (u64)(uintptr_t)bytes;
+  auto load = [&](u64 t, u64 &a, u64 &hi) {
+    const u64 k0 = t << 6;
+    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
+    a = offsets[(k0 + lane < n) ? k0 + lane : n];
+    hi = offsets[kend];
+  };
+  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
+  u64 a = 0, hi = 0;
+  if (t < ntiles) load(t, a, hi);
+  for (; t < ntiles; t += nwaves) {
+    const u64 i = (t << 6) + lane;
+    const bool valid = i < n;
+    const u64 nb = __shfl_down(a, 1);
+    const u64 start = a - obase;
+    const u64 end = (lane == 63 ? hi : nb) - obase;
+    // lane 0 holds offsets[k0]; readfirstlane returns int: widen through u32
+    const u64 first = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)a) |
+                       ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(a >> 32)) << 32)) - obase;
+    const u64 whi = hi - obase;
+    const u64 wlo = (base + first) & ~(u64)15;  // absolute, as in k_window
+    const u64 span = whi > first ? base + whi - wlo : 0;
+    const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)wlo);
+#pragma unroll
+    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
+      if ((u32)j * 1024 < wbytes) {  // wave-uniform
+        if ((u32)j * 1024 + lane * 16 < wbytes)
+          __builtin_amdgcn_global_load_lds(
+              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+              (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, AUX);
+      }
+    }
+    // the next tile's offsets travel with this tile's window
+    const u64 tn = t + nwaves;
+    if (tn < ntiles) load(tn, a, hi);  // wave-uniform
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+      const u64 len = end - start;
+      typename Algo::Out h;
+      if (base + end - wlo <= wbytes)
+        h = algo(LdsReader{lds, (u32)(base + start - wlo)}, len);
+      else
+        h = algo(GlobalReader{bytes + start}, len);
+      sink.put(i, h);
+    }
+    __builtin_amdgcn_wave_barrier();  // window reused by the next tile
+  }
+  sink.flush();
+}
+
+// ----------------------------------- double-buffered window kernel (var) ---
+// Offset-indexed keys with two LDS windows per wave: while tile t hashes out
+// of one window, the LDS-DMA of tile t+nwaves streams into the other, and
+// the offsets of tile t+2*nwaves are on their way.  The windows are two
+// distinct __shared__ objects and the loop is unrolled by two, so every LDS
+// read names its window.  A tile's digests are stored one step late, right
+// after the next DMA is issued, so the wait at the top of a step only covers
+// operations issued a whole tile of hashing earlier (on CDNA a load wait is
+// a vmcnt wait and also waits for every older store).  Window bounds are
+// absolute addresses, as in k_window.
+template <int WIN, class Algo, class Sink, int AUX = 2>
+__global__ __launch_bounds__(kBlock) void k_window_db(const uint8_t *__restrict__ bytes,
+                                                      const u64 *__restrict__ offsets, u64 obase, u64 n,
+                                                      Algo algo, Sink sink) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  __shared__ __attribute__((aligned(16))) u32 winA[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ __attribute__((aligned(16))) u32 winB[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  algo_init(algo);
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *const wa = winA + wave * (WIN / 4);
+  u32 *const wb = winB + wave * (WIN / 4);
+  const u64 base = (u64)(uintptr_t)bytes;
+  struct Geo {
+    u64 wlo, start, end;  // wlo absolute; start/end relative to bytes
+    u32 wbytes;
+  };
+  auto load_offs = [&](u64 t, u64 &a, u64 &hi) {
+    const u64 k0 = t << 6;
+    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
+    a = offsets[(k0 + lane < n) ? k0 + lane : n];
+    hi = offsets[kend];
+  };
+  auto geometry = [&](u64 a, u64 hi) {
+    Geo g;
+    const u64 nb = __shfl_down(a, 1);
+    g.start = a - obase;
+    g.end = (lane == 63 ? hi : nb) - obase;
+    // readfirstlane returns int: widen through u32 (no sign extension)
+    const u64 first = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)a) |
+                       ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(a >> 32)) << 32)) - obase;
+    const u64 whi = hi - obase;
+    g.wlo = (base + first) & ~(u64)15;
+    const u64 span = whi > first ? base + whi - g.wlo : 0;
+    g.wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    return g;
+  };
+  auto issue = [&](const Geo &g, u32 *w) {
+    const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)g.wlo);
+#pragma unroll
+    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
+      if ((u32)j * 1024 < g.wbytes) {  // wave-uniform
+        if ((u32)j * 1024 + lane * 16 < g.wbytes)
+          __builtin_amdgcn_global_load_lds(
+              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+              (void __attribute__((address_space(3))) *)(w + 256 * j), 16, 0, AUX);
+      }
+    }
+  };
+  typename Algo::Out h{};
+  u64 hi_pend = ~0ull;  // index of the digest held in h (~0: none)
+  auto hash = [&](u64 t, const Geo &g, const u32 *w) {
+    const u64 i = (t << 6) + lane;
+    hi_pend = ~0ull;
+    if (i < n) {
+      const u64 len = g.end - g.start;
+      if (base + g.end - g.wlo <= g.wbytes)
+        h = algo(LdsReader{w, (u32)(base + g.start - g.wlo)}, len);
+      else
+        h = algo(GlobalReader{bytes + g.start}, len);
+      hi_pend = i;
+    }
+  };
+  auto put_pending = [&] {
+    if (hi_pend != ~0ull) sink.put(hi_pend, h);
+  };
+  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
+  if (t < ntiles) {
+    u64 a, hi, an, hin;
+    load_offs(t, a, hi);
+    Geo g = geometry(a, hi), gn;
+    issue(g, wa);
+    // offsets loads are unconditional (clamped tile): a conditional load
+    // merges with the old value through a register copy, and the copy waits
+    // vmcnt(0) for the DMA issued just before it
+    const u64 last = ntiles - 1;
+    load_offs(min(t + nwaves, last), an, hin);
+    auto step = [&](u32 *cur, u32 *nxt) -> bool {
+      const u64 tn = t + nwaves;
+      const bool more = tn < ntiles;  // wave-uniform
+      // tile t's DMA (issued one step ago) has landed; the compiler does not
+      // order LDS reads after LDS-DMA by itself, so this wait is what makes
+      // `cur` readable (it also covers the offsets loads of the same step)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (more) {
+        gn = geometry(an, hin);
+        issue(gn, nxt);
+      }
+      put_pending();
+      if (more) load_offs(min(tn + nwaves, last), an, hin);
+      hash(t, g, cur);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // `cur` is the DMA target two tiles on
+      g = gn;
+      t = tn;
+      return more;
+    };
+    while (step(wa, wb) && step(wb, wa)) {
+    }
+    put_pending();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sink.flush();
+}
+
 // ---------------------------------------------------------- long keys ---
 // Keys far longer than a 64-key LDS window can hold (fixed L > 255 B): each
 // lane walks its own key straight from global memory (GlobalReader); the
 // other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
 // bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
-template <bool VAR, class Algo, class Sink>
+template <bool VAR, class Algo, class Sink, bool A16 = false>
 __global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -573,7 +812,7 @@ __global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ b
       st = i * stride;
       len = keylen;
     }
-    sink.put(i, algo(GlobalReader{bytes + st}, len));
+    sink.put(i, algo(GlobalReaderT<A16>{bytes + st}, len));
   }
   sink.flush();
 }

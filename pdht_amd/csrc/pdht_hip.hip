@@ -195,9 +195,15 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
       // keys too long for a 64-key window: per-lane global reads (r01: an
       // LDS chunk-streaming kernel measured 0.36-0.47 of peak against this
       // kernel's 0.50-0.62 on 256 B - 8 KiB keys)
-      g_kernel = "k_global<fixed>@8";
-      k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(k, nullptr, 0, stride,
-                                                                                  keylen, n, algo, sink_nt);
+      if (al16 && stride % 16 == 0) {
+        g_kernel = "k_global<fixed,a16>@8";
+        k_global<false, Algo, SinkNt, true><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+      } else {
+        g_kernel = "k_global<fixed>@8";
+        k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(k, nullptr, 0, stride,
+                                                                                    keylen, n, algo, sink_nt);
+      }
     } else if (tile_bytes > kWinBytes) {
       g_kernel = "k_window<fixed,nt,16K>@2";
       k_window<16384, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 2, dev), kBlock, 0, st>>>(
@@ -234,6 +240,43 @@ static int launch_var(const void *bytes, u64 nbytes, const u64 *offsets, u64 oba
 #ifdef PDHT_HIP_TUNING
   if (tuning_variant() == 12) wide = false;
   if (tuning_variant() == 13) wide = true;
+  if (tuning_variant() == 46) {  // windows start on a 128-B line
+    g_kernel = "k_window<var,nt,10224,a128>@4";
+    k_window<10224, true, Algo, SinkNt, 2, 128><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0,
+                                                                                       n, algo, sink_nt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (tuning_variant() >= 23 && tuning_variant() <= 25) {  // double-buffered windows
+    if (tuning_variant() == 23) {
+      g_kernel = "k_window_db<10224>@2";
+      k_window_db<10224, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                 sink_nt);
+    } else if (tuning_variant() == 24) {
+      g_kernel = "k_window_db<6656>@3";
+      k_window_db<6656, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                sink_nt);
+    } else {
+      g_kernel = "k_window_db<8192>@2";
+      k_window_db<8192, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                sink_nt);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (tuning_variant() == 30 || tuning_variant() == 31) {  // offsets prefetched one tile ahead
+    if (tuning_variant() == 31 || wide) {
+      g_kernel = "k_window_var<16K>@2";
+      k_window_var<16384, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                  sink_nt);
+    } else {
+      g_kernel = "k_window_var<10224>@4";
+      k_window_var<10224, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                  sink_nt);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
 #endif
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";
@@ -812,6 +855,43 @@ PDHT_API int pdht_hip_key_stream_dev(const void *keys, size_t n, uint64_t *out,
 PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
                                          size_t n, uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
+#ifdef PDHT_HIP_TUNING
+  // data-movement calibrations of the window kernel (no LDS reads, digest =
+  // key length): 40 as shipped; 41 default-policy DMA; 42 plain stores;
+  // 43 as 40 at 3 WG/CU; 44 offsets prefetched (k_window_var)
+  const int v = tuning_variant();
+  if (v >= 40 && v <= 45) {
+    if (n == 0) return 0;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    const uint8_t *b = static_cast<const uint8_t *>(bytes);
+    const u64 wb = ((n + 63) / 64 + 3) / 4;
+    const Sink64T<true> snt{nullptr, out};
+    const Sink64 spl{nullptr, out};
+    hipStream_t st = ST(s);
+    g_kernel = "k_window<var,calib>";
+    if (v == 40)
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else if (v == 41)
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 0><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else if (v == 42)
+      k_window<10224, true, AlgoLenOnly, Sink64, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, spl);
+    else if (v == 43)
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else if (v == 45)  // windows start on a 128-B line
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2, 128><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else
+      k_window_var<10224, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, n, AlgoLenOnly{}, snt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+#endif
   return launch_var(bytes, nbytes, offsets, 0, n, AlgoFoldVar{}, Sink64{nullptr, out}, ST(s));
 }
 
@@ -881,15 +961,17 @@ struct BucketArgs {
   u64 ntiles;
 };
 
-template <int L, class Out>
+template <int L, class Out, bool PACK = false>
 static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
-  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
-  const size_t bytes = staged_lds_bytes(a.nranks);
-  auto fn = &k_bucket_scatter_staged<L, Out>;
+  static const char *const pnames[3] = {"k_bucket_scatter_staged<8B,u16>", "k_bucket_scatter_staged<16B,u16>",
+                                        "k_bucket_scatter_staged<32B,u16>"};
+  g_kernel = (PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = staged_lds_bytes(a.nranks, kStW, kStKPL, PACK);
+  auto fn = &k_bucket_scatter_staged<L, Out, kStW, kStKPL, PACK>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
-  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
+  const int per_cu = bytes <= 53 * 1024 ? 3 : bytes <= 80 * 1024 ? 2 : 1;
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
   fn<<<g, kStW * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
@@ -986,6 +1068,13 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
+#ifdef PDHT_HIP_TUNING
+    if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
+      rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
+                           : launch_staged<32, Out, true>(a, out, st, dev);
+    else
+#endif
     if (kind == BucketKernel::kStaged)
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)

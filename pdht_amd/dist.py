@@ -145,6 +145,44 @@ def exchange_records(records, offsets):
     return out.view(-1, rb), recv
 
 
+def device_info(device=None) -> dict:
+    """Where this rank runs: host, device index, name and PCI address (the
+    RCCL world / device map of a multi-GPU bench line)."""
+    import socket
+    info = {"host": socket.gethostname()}
+    if device is not None and getattr(device, "type", "cpu") == "cuda":
+        import torch
+        p = torch.cuda.get_device_properties(device)
+        info.update(device=device.index, name=p.name,
+                    pci=f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                        f"{getattr(p, 'pci_device_id', 0):02x}")
+    else:
+        info.update(device=None, name="cpu", pci=None)
+    return info
+
+
+def per_rank_report(rank: int, local: int, world: int, n: int, bytes_per_key: float, kernel_ms: float,
+                    elapsed_s: float, steps: int, peak_GBps: float, device=None) -> dict:
+    """Every rank's own numbers, gathered to all ranks: device, kernel time,
+    Gkeys/s and roofline fraction per GPU, plus the world (SURVEY.md §8e:
+    per-GPU and aggregate Gkeys/s at 1/2/4/8 GPUs)."""
+    import torch.distributed as dist
+    mine = dict(rank=rank, local_rank=local, **device_info(device),
+                kernel_ms=round(kernel_ms, 4),
+                Gkeys_s=round(n / (kernel_ms / 1e3) / 1e9, 3),
+                frac=round(bytes_per_key * n / (kernel_ms / 1e3) / 1e9 / peak_GBps, 4),
+                wall_Gkeys_s=round(n * steps / elapsed_s / 1e9, 3))
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        allr = [None] * dist.get_world_size()
+        dist.all_gather_object(allr, mine)
+        backend = dist.get_backend()
+    else:
+        allr, backend = [mine], None
+    return {"world_size": len(allr), "backend": backend, "ranks": allr,
+            "Gkeys_s": [r["Gkeys_s"] for r in allr], "frac": [r["frac"] for r in allr],
+            "aggregate_kernel_Gkeys_s": round(sum(r["Gkeys_s"] for r in allr), 3)}
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:

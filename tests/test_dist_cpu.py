@@ -68,8 +68,11 @@ def _worker(rank, world, port, q):
         rec[:, 16:24] = mb[order].view(np.uint8).reshape(-1, 8)
         rec[:, 24:32] = keys[order, :8]
         xr, xrc = D.exchange_records(torch.from_numpy(rec), torch.from_numpy(offs.astype(np.int64)))
+        # the N > 1 bench line's per-rank block (bench.py per_rank): rank r
+        # reports a kernel time of (r+1) ms for its n keys
+        pr = D.per_rank_report(r, lr, w, 1 << 20, 72, float(r + 1), 2.0, 10, 8000.0)
         D.barrier()
-        q.put({"rank": r, "first": sh.first, "n": sh.n, "local": local, "total": total,
+        q.put({"rank": r, "first": sh.first, "n": sh.n, "local": local, "total": total, "per_rank": pr,
                "xrec": xr.numpy(), "xrcnt": xrc.numpy(),
                "max": mx, "ok_all": ok_all,
                "oracle_local": O.fold64(O.city64_fixed(keys), sh.first),
@@ -113,6 +116,14 @@ def test_two_rank_gloo_shards_and_reductions(oracle):
         assert r["total"] == want_total                 # and they add up to the whole
         assert r["max"] == [float(WORLD), 0.5 * (WORLD - 1)]
         assert r["ok_all"] is False                     # one failing rank fails all
+        pr = r["per_rank"]                              # every rank sees every rank's numbers
+        assert pr["world_size"] == WORLD and pr["backend"] == "gloo"
+        assert [x["rank"] for x in pr["ranks"]] == list(range(WORLD))
+        assert all({"host", "device", "name", "pci", "kernel_ms", "Gkeys_s", "frac", "wall_Gkeys_s"} <= set(x)
+                   for x in pr["ranks"])
+        assert pr["Gkeys_s"] == [round((1 << 20) / (k + 1) / 1e6, 3) for k in range(WORLD)]
+        assert pr["frac"] == [round(72 * (1 << 20) / (k + 1) / 1e6 / 8000, 4) for k in range(WORLD)]
+        assert pr["aggregate_kernel_Gkeys_s"] == round(sum(pr["Gkeys_s"]), 3)
     # after the exchange rank r holds exactly the keys the reference places on r,
     # grouped by source rank, each group in key order
     mb, _, rk = oracle.pdht_hash_fixed(whole[:, :8], 3, WORLD)

@@ -8,8 +8,12 @@ LDS-DMA alike) -> x2.  WRITE_SIZE is exact for streaming stores.  Both are in
 KiB.
 
   python tools/pmc_traffic.py --cfg cfg2 --keys 16777216 --kernel k_fixed_xpose64 \
-      --dir gpurun_out --out profiles/traffic_cfg2.json
+      --algo-bytes-per-key 72 --fetch-dir gpurun_out/pmc_cfg2_1 --write-dir gpurun_out/pmc_cfg2_2 \
+      --bench-log gpurun_out/pmc_cfg2_1.log --out profiles/traffic_cfg2.json
   (--kernel "a|b|c" sums several kernels of one step, e.g. the bucketing launches)
+The kernel tag of the run (pdht_hip_last_kernel, from the bench line in
+--bench-log) and the full rocprof kernel symbols are stored: bench.py uses
+the figure only when the tag of ITS kernel is the same.
 """
 import argparse
 import csv
@@ -19,11 +23,14 @@ import statistics
 
 
 def per_launch(path, kernel, counter):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+    rows = [r for r in csv.DictReader(open(path))
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    if not vals:
+    if not rows:
         raise SystemExit(f"no {counter} rows for {kernel} in {path}")
-    return statistics.median(vals), len(vals)
+    names = sorted({r["Kernel_Name"] for r in rows})
+    if len(names) != 1:
+        raise SystemExit(f"{kernel} matches several kernels in {path}: {names}")
+    return statistics.median(float(r["Counter_Value"]) for r in rows), len(rows), names[0]
 
 
 def main():
@@ -36,21 +43,29 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--fetch-dir", default=None, help="default: <dir>/pmc_FETCH_SIZE")
     ap.add_argument("--write-dir", default=None, help="default: <dir>/pmc_WRITE_SIZE")
+    ap.add_argument("--bench-log", required=True, help="bench.py output of the profiled run (kernel tag)")
     a = ap.parse_args()
     fd = a.fetch_dir or os.path.join(a.dir, "pmc_FETCH_SIZE")
     wd = a.write_dir or os.path.join(a.dir, "pmc_WRITE_SIZE")
     # --kernel "a|b|c": the step launches several kernels; sum their medians
     f_kib = w_kib = 0.0
     nf = nw = 0
+    symbols = []
     for k in a.kernel.split("|"):
-        f, nf = per_launch(os.path.join(fd, "run_counter_collection.csv"), k, "FETCH_SIZE")
-        w, nw = per_launch(os.path.join(wd, "run_counter_collection.csv"), k, "WRITE_SIZE")
+        f, nf, name = per_launch(os.path.join(fd, "run_counter_collection.csv"), k, "FETCH_SIZE")
+        w, nw, name2 = per_launch(os.path.join(wd, "run_counter_collection.csv"), k, "WRITE_SIZE")
+        if name != name2:
+            raise SystemExit(f"FETCH and WRITE passes profiled different kernels: {name} / {name2}")
+        symbols.append(name)
         f_kib += f
         w_kib += w
+    line = [ln for ln in open(a.bench_log) if ln.startswith("{")][-1]
+    tag = json.loads(line)["config"]["kernel"]
     fetch = f_kib * 1024 * 2  # gfx950: FETCH_SIZE = half of a wide streaming read
     write = w_kib * 1024
     algo = a.algo_bytes_per_key * a.keys
-    res = {"cfg": a.cfg, "kernel": a.kernel, "keys_per_launch": a.keys,
+    res = {"cfg": a.cfg, "kernel": a.kernel, "kernel_tag": tag, "rocprof_kernels": symbols,
+           "keys_per_launch": a.keys,
            "fetch_size_kib_raw": f_kib, "fetch_correction": 2, "write_size_kib_raw": w_kib,
            "launches_sampled": [nf, nw],
            "hbm_bytes_per_launch": int(fetch + write),
