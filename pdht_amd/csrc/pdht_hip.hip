@@ -1000,7 +1000,27 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
   return 0;
 }
 
-enum class BucketKernel { kStaged, kReg, kGeneric };
+#ifdef PDHT_HIP_TUNING
+template <int W, int KPL, class Out>
+static int launch_gather(const BucketArgs &a, const Out &out, u32 L, int lk, hipStream_t st, int dev) {
+  const size_t bytes = gather_lds_bytes(a.nranks, W, KPL);
+  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
+  auto go = [&](auto fn, const char *name) -> int {
+    g_kernel = name;
+    if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
+    unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
+    if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
+    fn<<<g, W * 64, bytes, st>>>(a.k, L, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+    return 0;
+  };
+  if (lk == 8) return go(&k_bucket_scatter_gather<8, Out, W, KPL>, "k_bucket_scatter_gather<8B>");
+  if (lk == 16) return go(&k_bucket_scatter_gather<16, Out, W, KPL>, "k_bucket_scatter_gather<16B>");
+  if (lk == 32) return go(&k_bucket_scatter_gather<32, Out, W, KPL>, "k_bucket_scatter_gather<32B>");
+  return go(&k_bucket_scatter_gather<0, Out, W, KPL>, "k_bucket_scatter_gather<any>");
+}
+#endif
+
+enum class BucketKernel { kGather, kStaged, kReg, kGeneric };
 
 // Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
 // (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
@@ -1023,18 +1043,28 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   // 2048 ranks, register scatter above; other lengths -> generic.
   const uintptr_t al = (uintptr_t)keys | out_al;
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
-  BucketKernel kind = !fixed ? BucketKernel::kGeneric
+  BucketKernel kind = !fixed                     ? BucketKernel::kGeneric
                       : nranks > kStagedMaxRanks ? BucketKernel::kReg
                                                  : BucketKernel::kStaged;
+  int ga_w = kGaW, ga_kpl = kGaKPL;
 #ifdef PDHT_HIP_TUNING
+  // 21 generic, 22 register scatter; 54 the gather scatter (16384-key tiles,
+  // keys gathered back from L2 and re-hashed), 52 / 53 it with 8192-key
+  // tiles (4 waves x 32 / 8 waves x 16 keys per lane); 55-57 its timing-only
+  // builds; 58 producer/consumer scatter; 50 staged with u16 run tables.
+  // All measured slower than the staged scatter.
   if (tuning_variant() == 21) kind = BucketKernel::kGeneric;
   if (tuning_variant() == 22 && fixed) kind = BucketKernel::kReg;
+  if (tuning_variant() >= 52 && tuning_variant() <= 58 && nranks <= kStagedMaxRanks) kind = BucketKernel::kGather;
+  if (tuning_variant() == 52) ga_w = 4;
+  if (tuning_variant() == 53) ga_kpl = 16;
 #endif
   const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
   const int reg_kpl = keysize == 32 ? 8 : 16;
-  const u64 tile = kind == BucketKernel::kStaged ? kStTile
-                   : kind == BucketKernel::kReg  ? (u64)waves * reg_kpl * 64
-                                                 : (u64)waves * kScatKPL * 64;
+  const u64 tile = kind == BucketKernel::kGather   ? (u64)ga_w * ga_kpl * 64
+                   : kind == BucketKernel::kStaged ? kStTile
+                   : kind == BucketKernel::kReg    ? (u64)waves * reg_kpl * 64
+                                                   : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   BucketArgs a{};
@@ -1068,8 +1098,37 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
+    const int lk = fixed ? (int)keysize : 0;
 #ifdef PDHT_HIP_TUNING
-    if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
+    if (kind == BucketKernel::kGather && !(tuning_variant() >= 55 && tuning_variant() <= 58 && lk == 8)) {
+      if (ga_w == 8 && ga_kpl == 32)
+        rc = launch_gather<8, 32>(a, out, (u32)keysize, lk, st, dev);
+      else if (ga_w == 4)
+        rc = launch_gather<4, 32>(a, out, (u32)keysize, lk, st, dev);
+      else
+        rc = launch_gather<8, 16>(a, out, (u32)keysize, lk, st, dev);
+    } else if (kind == BucketKernel::kGather && lk == 8 && tuning_variant() == 58) {
+      // producer/consumer scatter: 8 + 8 waves, 16384-key tiles, 1 WG/CU
+      const size_t bytes = (size_t)8 * a.nranks * 4 + (size_t)2 * a.nranks * 4 + (size_t)2 * 16384 * 2;
+      auto fn = &k_bucket_scatter_pc<Out, 8, 32>;
+      g_kernel = "k_bucket_scatter_pc<8B>";
+      if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
+      unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus));
+      if (g >= 8) g &= ~7u;
+      fn<<<g, 1024, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+    } else if (kind == BucketKernel::kGather && ga_w == 8 && ga_kpl == 32 && lk == 8 &&
+               tuning_variant() >= 55 && tuning_variant() <= 57) {
+      // timing-only builds (wrong results): 55 no stores, 56 no gather, 57 no phase D
+      const size_t bytes = gather_lds_bytes(a.nranks, 8, 32);
+      const int v = tuning_variant();
+      auto fn = v == 55 ? &k_bucket_scatter_gather<8, Out, 8, 32, 32, 1>
+                : v == 56 ? &k_bucket_scatter_gather<8, Out, 8, 32, 32, 2>
+                          : &k_bucket_scatter_gather<8, Out, 8, 32, 32, 4>;
+      g_kernel = "k_bucket_scatter_gather<8B,timing-only>";
+      if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
+      unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * 2) & ~7u;
+      fn<<<g, 512, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+    } else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
       rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
                            : launch_staged<32, Out, true>(a, out, st, dev);

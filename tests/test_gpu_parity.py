@@ -425,15 +425,27 @@ BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1
                 for n in (0, 1, 4095, 100003)]
 BUCKET_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192)
                  for n in (4095, 300007)]
+BUCKET_CASES += [(L, nr, n, v) for v in (54, 58) for L in (8, 13, 16) for nr in (7, 1000, 2048)
+                 for n in (1, 16383, 16385, 1 << 20)]
 
 
 def _bucket_kernel(L, nranks, variant):
-    """Tuning variants: 21 forces the generic-length kernel, 22 the register
-    (unstaged) one."""
-    if variant != 21 and L in (8, 16, 32):
-        kind = "reg" if variant == 22 or nranks > 2048 else "staged"
-        return f"k_bucket_scatter_{kind}<{L}B>"
-    return "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
+    """Product: the staged scatter for 8/16/32-B keys up to 2048 ranks, the
+    register scatter above, the generic one for other lengths.  Tuning
+    variants: 21 forces the generic-length kernel, 22 the register one, 54 the
+    gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys)."""
+    wg = "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
+    if variant == 21:
+        return wg
+    if variant == 22 and L in (8, 16, 32):
+        return f"k_bucket_scatter_reg<{L}B>"
+    if variant == 58 and L == 8 and nranks <= 2048:
+        return "k_bucket_scatter_pc<8B>"
+    if variant in (54, 58) and nranks <= 2048:
+        return f"k_bucket_scatter_gather<{L}B>" if L in (8, 16, 32) else "k_bucket_scatter_gather<any>"
+    if L in (8, 16, 32):
+        return f"k_bucket_scatter_{'staged' if nranks <= 2048 else 'reg'}<{L}B>"
+    return wg
 
 
 @pytest.mark.parametrize("L,nranks,n,variant", BUCKET_CASES)
@@ -478,7 +490,7 @@ def test_bucket_optional_outputs(dev, oracle, L):
 
 RECORD_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 7, 1000, 2049, 8192)
                 for n in (0, 1, 4095, 100003)]
-RECORD_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2048)
+RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 54, 58) for L in (8, 16, 32) for nr in (7, 1000, 2048)
                  for n in (4097, 300007)]
 
 

@@ -35,7 +35,9 @@ typedef unsigned int u32;
 // R bytes per run, written as R/4 dwords; 256 threads cover a tile's
 // nranks runs: thread j writes dword j, j+256, ... of the tile's
 // nranks*R/4 dwords (run r = dwords [r*R/4, (r+1)*R/4)).
-__global__ __launch_bounds__(256) void scatter(u32 *__restrict__ out, u32 R4, u32 nranks, u64 ntiles) {
+// skew4: every run is shifted by skew4 dwords (runs of a real counting sort
+// start wherever the prefix sums put them, not on a line).
+__global__ __launch_bounds__(256) void scatter(u32 *__restrict__ out, u32 R4, u32 nranks, u64 ntiles, u32 skew4) {
   u64 t, end, step;
   if (gridDim.x >= 8 && gridDim.x % 8 == 0) {
     const u64 x = blockIdx.x % 8, per = gridDim.x / 8;
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(256) void scatter(u32 *__restrict__ out, u32 R4, u3
   for (; t < end; t += step) {
     for (u32 d = threadIdx.x; d < nd; d += 256) {
       const u32 r = d / R4, k = d - r * R4;
-      out[((u64)r * ntiles + t) * R4 + k] = (u32)t ^ d;
+      out[((u64)r * ntiles + t) * R4 + k + skew4] = (u32)t ^ d;
     }
   }
 }
@@ -66,19 +68,21 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   const u32 Rs[] = {16, 32, 64, 128, 256};
-  const u32 NRs[] = {1024, 256, 64};
-  const int PCs[] = {2, 4, 8};
+  const u32 NRs[] = {1024};
+  const int PCs[] = {2};
+  const u32 SKs[] = {0, 2, 7};  // dwords
+  for (u32 sk : SKs)
   for (u32 nr : NRs)
     for (u32 R : Rs)
       for (int pc : PCs) {
         const u64 ntiles = total / ((u64)R * nr);
         const unsigned g = (unsigned)std::min<u64>(ntiles, (u64)cus * pc) & ~7u;
-        scatter<<<g, 256>>>(buf, R / 4, nr, ntiles);
+        scatter<<<g, 256>>>(buf, R / 4, nr, ntiles - 1, sk);
         CK(hipDeviceSynchronize());
         std::vector<float> ms;
         for (int i = 0; i < 10; ++i) {
           CK(hipEventRecord(a));
-          scatter<<<g, 256>>>(buf, R / 4, nr, ntiles);
+          scatter<<<g, 256>>>(buf, R / 4, nr, ntiles - 1, sk);
           CK(hipEventRecord(b));
           CK(hipEventSynchronize(b));
           float m;
@@ -87,9 +91,9 @@ int main(int argc, char **argv) {
         }
         std::sort(ms.begin(), ms.end());
         const double bytes = (double)ntiles * R * nr;
-        printf("{\"run_bytes\": %u, \"nranks\": %u, \"per_cu\": %d, \"MiB\": %.0f, \"median_ms\": %.4f, "
-               "\"GBps\": %.1f}\n",
-               R, nr, pc, bytes / 1048576, ms[5], bytes / ms[5] / 1e6);
+        printf("{\"run_bytes\": %u, \"skew_bytes\": %u, \"nranks\": %u, \"per_cu\": %d, \"MiB\": %.0f, "
+               "\"median_ms\": %.4f, \"GBps\": %.1f}\n",
+               R, 4 * sk, nr, pc, bytes / 1048576, ms[5], bytes / ms[5] / 1e6);
       }
   CK(hipFree(buf));
   return 0;
