@@ -117,7 +117,7 @@ def main():
         words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
         nr = 1024 if cfg == "records" else world
-        ws = torch.empty(P.bucket_workspace_bytes(n, nr), dtype=torch.uint8, device=dev)
+        ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
         recs = P.bucket_records(keys, nr, src_rank=rank, workspace=ws)
         bucketed = {"nranks": nr, "records": True}
 
@@ -143,9 +143,11 @@ def main():
         keys = words.view(torch.uint8).view(n, L)
         nr = 1024 if cfg == "bucket" else world
         bucketed = {"nranks": nr}
+        ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
+        bk = P.bucket_batch(keys, 3, nr, with_ptindex=cfg == "bucket", workspace=ws)
 
         def step():
-            ko, mb, pt, ix, offs_ = P.bucket_batch(keys, 3, nr, with_ptindex=cfg == "bucket")
+            ko, mb, pt, ix, offs_ = P.bucket_batch(keys, 3, nr, out=bk, workspace=ws)
             bucketed.update(ko=ko, mb=mb, pt=pt, ix=ix, offs=offs_)
             if cfg == "exchange" and world > 1:
                 bucketed["x"] = D.exchange_buckets(ko, mb, offs_, (ix.long() & 0xFFFFFFFF) + sh.first)

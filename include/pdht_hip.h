@@ -113,8 +113,10 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * holding index_out can gather keys itself and pass keys_out = NULL; with
  * nptes == 1 (pdht's default, pdht_impl.h:41) every ptindex is 0 and
  * ptindex_out is best NULL.  nranks <= 8192, n < 2^32.  `workspace`
- * (device) must hold pdht_bucket_workspace_bytes. */
-size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks);
+ * (device) must hold pdht_bucket_workspace_bytes(n, keysize, nranks): the
+ * per-tile counts and, for 8/16/32-B keys, the intermediate of the two-pass
+ * sort used from 256 ranks up (n x (keysize + 4) bytes). */
+size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint32_t nptes, uint32_t nranks, void *workspace,
                           size_t workspace_bytes, void *keys_out,

@@ -107,7 +107,7 @@ def _declare(L, tuning=False):
         "pdht_hip_read_stream_dev": (C.c_int, [_V, _S, C.c_int, _V, _V]),
         "pdht_hip_key_stream_dev": (C.c_int, [_V, _S, _V, _V]),
         "pdht_hip_key_stream_var_dev": (C.c_int, [_V, _S, _V, _S, _V, _V]),
-        "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _U32]),
+        "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _S, _U32]),
         "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
         "pdht_bucket_record_bytes": (C.c_size_t, [_S]),
         "pdht_bucket_records_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _U32, _U32, _V, _S, _V, _V, _V]),
@@ -484,13 +484,13 @@ def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=
     return mb, pt, rk
 
 
-def bucket_workspace_bytes(n: int, nranks: int) -> int:
-    return lib().pdht_bucket_workspace_bytes(n, nranks)
+def bucket_workspace_bytes(n: int, keysize: int, nranks: int) -> int:
+    return lib().pdht_bucket_workspace_bytes(n, keysize, nranks)
 
 
-def _workspace(workspace, n, nranks, dev):
+def _workspace(workspace, n, L, nranks, dev):
     torch = _torch()
-    need = lib().pdht_bucket_workspace_bytes(n, nranks)
+    need = lib().pdht_bucket_workspace_bytes(n, L, nranks)
     if workspace is None:
         return torch.empty(max(need, 1), dtype=torch.uint8, device=dev), need
     _need(workspace, "workspace", torch.uint8, dev, numel=need)
@@ -507,14 +507,14 @@ def bucket_batch(keys, nptes: int, nranks: int, *, with_keys=True, with_ptindex=
     int64[nranks+1]); bucket r is rows offsets[r]:offsets[r+1], keys in
     original order.  `out` = a previous return value (same n, L, nranks) to
     reuse its tensors; `workspace` = a uint8 CUDA tensor of at least
-    bucket_workspace_bytes(n, nranks) bytes (allocated per call if None).
+    bucket_workspace_bytes(n, L, nranks) bytes (allocated per call if None).
     """
     torch = _torch()
     n, L, stride = _keys_2d(keys)
     if stride != L:
         raise ValueError("bucket_batch needs packed keys")
     dev = keys.device
-    ws, ws_bytes = _workspace(workspace, n, nranks, dev)
+    ws, ws_bytes = _workspace(workspace, n, L, nranks, dev)
     if out is not None:
         ko, mb, pt, ix, offs = out
         if ko is not None:
@@ -561,7 +561,7 @@ def bucket_records(keys, nranks: int, *, msg_type: int = PDHT_PUT, src_rank: int
         raise ValueError("bucket_records needs packed keys")
     dev = keys.device
     rb = bucket_record_bytes(L)
-    ws, ws_bytes = _workspace(workspace, n, nranks, dev)
+    ws, ws_bytes = _workspace(workspace, n, L, nranks, dev)
     if out is not None:
         rec, offs = out
         _need(rec, "out[0] (records)", torch.uint8, dev, shape=(n, rb))

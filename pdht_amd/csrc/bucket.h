@@ -158,36 +158,6 @@ __global__ __launch_bounds__(kBlock) void k_bucket_chunkscan(u32 *__restrict__ c
   totals[r] = run;
 }
 
-// Exclusive scan of the per-rank totals (one workgroup) -> bucket offsets.
-__global__ __launch_bounds__(kBlock) void k_bucket_base(const u64 *__restrict__ totals, u32 nranks,
-                                                        u64 *__restrict__ base,
-                                                        u64 *__restrict__ offsets_out) {
-  __shared__ u64 part[kBlock];
-  const u32 per = (nranks + kBlock - 1) / kBlock;
-  const u32 lo = threadIdx.x * per;
-  const u32 hi = (lo + per < nranks) ? lo + per : nranks;
-  u64 s = 0;
-  for (u32 r = lo; r < hi; ++r) s += totals[r];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    u64 run = 0;
-    for (int k = 0; k < kBlock; ++k) {
-      const u64 v = part[k];
-      part[k] = run;
-      run += v;
-    }
-    offsets_out[nranks] = run;
-  }
-  __syncthreads();
-  u64 run = part[threadIdx.x];
-  for (u32 r = lo; r < hi; ++r) {
-    base[r] = run;
-    offsets_out[r] = run;
-    run += totals[r];
-  }
-}
-
 // ------------------------------------------------------------- helpers ---
 // Lanes whose r equals mine (AND of per-bit ballots; invalid lanes excluded).
 __device__ __forceinline__ u64 same_bucket_lanes(bool valid, u32 r, u32 nbits) {
@@ -206,18 +176,18 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Exclusive scan of one value per thread over an NW-wave workgroup.
-template <int NW>
-__device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW words */) {
+template <int NW, class T = u32>
+__device__ __forceinline__ T block_exclusive_scan(T v, T *scratch /* NW words */) {
   const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  u32 x = v;
+  T x = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const u32 y = __shfl_up(x, d);
+    const T y = __shfl_up(x, d);
     if (lane >= (u32)d) x += y;
   }
   if (lane == 63) scratch[wave] = x;
   __syncthreads();
-  u32 off = 0;
+  T off = 0;
 #pragma unroll
   for (u32 w = 0; w < (u32)NW; ++w)
     if (w < wave) off += scratch[w];
@@ -231,6 +201,48 @@ __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32 *scratch /* NW wo
 // halves the table's LDS (16 -> 8 KiB at 1024 ranks).  Wave w's counters
 // start at w * stride (stride = nranks, rounded up to even when packed so a
 // word never straddles two waves).
+// Exclusive scan of the per-rank totals (one workgroup of kBaseThreads, each
+// thread a run of consecutive ranks) -> bucket offsets; with fbase (two-pass
+// bucketing), also the first intermediate row of every fine bucket f = r mod
+// F: the exclusive scan over f of the keys with r mod F == f.
+constexpr u32 kBaseThreads = 1024;
+__global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restrict__ totals, u32 nranks,
+                                                              u64 *__restrict__ base,
+                                                              u64 *__restrict__ offsets_out, u32 fbits,
+                                                              u64 *__restrict__ fbase) {
+  __shared__ u64 scratch[kBaseThreads / 64];
+  constexpr u32 kMaxPer = kBucketMaxRanks / kBaseThreads;
+  const u32 per = (nranks + kBaseThreads - 1) / kBaseThreads;
+  const u32 lo = min(threadIdx.x * per, nranks), hi = min(lo + per, nranks);
+  u64 v[kMaxPer];
+  u64 s = 0;
+#pragma unroll
+  for (u32 k = 0; k < kMaxPer; ++k) {
+    v[k] = lo + k < hi ? totals[lo + k] : 0;
+    s += v[k];
+  }
+  u64 run = block_exclusive_scan<kBaseThreads / 64, u64>(s, scratch);
+#pragma unroll
+  for (u32 k = 0; k < kMaxPer; ++k)
+    if (lo + k < hi) {
+      base[lo + k] = run;
+      offsets_out[lo + k] = run;
+      run += v[k];
+    }
+  if (hi == nranks && lo < hi) offsets_out[nranks] = run;
+  if (nranks == 0 && threadIdx.x == 0) offsets_out[0] = 0;
+  if (fbase) {
+    const u32 F = 1u << fbits;  // <= kTpMaxDigits
+    u64 fs = 0;
+    if (threadIdx.x < F)
+      for (u32 r = threadIdx.x; r < nranks; r += F) fs += totals[r];
+    __syncthreads();  // scratch reuse
+    const u64 fb = block_exclusive_scan<kBaseThreads / 64, u64>(fs, scratch);
+    if (threadIdx.x < F) fbase[threadIdx.x] = fb;
+  }
+}
+
+
 template <bool PACK>
 struct RunTab {
   u32 *t;
@@ -409,6 +421,65 @@ struct OutRec {
   }
 };
 
+// Phase D/E of the staged scatters: thread j writes staged entry j (digest in
+// stage[j]) to slot delta[digit(h)] + j with original index idx(j); then the
+// key rows, 8 bytes at a time through the same staging buffer (lp = each
+// held key's staged slot).  Stores are runs of consecutive lanes.
+template <int L, int KPL, u32 kB, class Out, class Dig, class Idx>
+__device__ __forceinline__ void staged_store(u64 *stage, const u32 *delta, u32 tn, const RegReader<L / 4> (&kr)[KPL],
+                                             const u32 (&lp)[KPL], u32 q0, const Dig &dig, const Idx &idx,
+                                             const Out &out) {
+  constexpr int kPer = KPL;  // entries per thread: a tile is kB x KPL keys
+  u32 gp[kPer];
+  if constexpr (Out::kPair8 && L == 8) {
+    // 8-B keys into 32-B records: two 16-B stores per record, {header,
+    // index} and {mbits, key}, half the store instructions of four 8-B ones
+    u64 hv[kPer];
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 j = min(jj * kB + threadIdx.x, tn - 1);
+      hv[jj] = stage[j];
+      gp[jj] = delta[dig(hv[jj])] + j;
+      if (jj * kB + threadIdx.x < tn) out.head(gp[jj], idx(j));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < KPL; ++g)
+      if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 j = jj * kB + threadIdx.x;
+      if (j < tn) out.tail8(gp[jj], hv[jj], stage[j]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int jj = 0; jj < kPer; ++jj) {
+    const u32 j = jj * kB + threadIdx.x;
+    if (j < tn) {
+      const u64 hv = stage[j];
+      gp[jj] = delta[dig(hv)] + j;
+      out.meta(gp[jj], hv, idx(j));
+    }
+  }
+  if (out.has_keys()) {
+#pragma unroll
+    for (int c = 0; c < L / 8; ++c) {
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < KPL; ++g)
+        if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
+      __syncthreads();
+#pragma unroll
+      for (int jj = 0; jj < kPer; ++jj) {
+        const u32 j = jj * kB + threadIdx.x;
+        if (j < tn) out.key8(gp[jj], c, stage[j]);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------ staged scatter ---
 // Tile = 4 waves x 16 groups x 64 lanes = 4096 keys; wave w owns the
 // contiguous quarter [w*1024, (w+1)*1024).
@@ -497,55 +568,252 @@ void k_bucket_scatter_staged(
         sidx[lp[g]] = (uint16_t)(q0 + g * 64);
       }
     __syncthreads();
-    constexpr int kPer = kTile / kB;
-    u32 gp[kPer];
-    if constexpr (Out::kPair8 && L == 8) {
-      // 8-B keys into 32-B records: two 16-B stores per record, {header,
-      // index} and {mbits, key}, half the store instructions of four 8-B ones
-      u64 hv[kPer];
+    staged_store<L, KPL, kB>(
+        stage, delta, tn, kr, lp, q0, [&](u64 hv) { return (u32)rk.mod(hv); },
+        [&](u32 j) { return tbase + sidx[j]; }, out);
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------- two-pass bucketing ---
+// One pass writes, per 4096-key tile, one run per bucket into every output
+// array: at 1024 ranks runs of 4 keys (32 B of an 8-B array, 16 B of a 4-B
+// one), and the write path runs at ~1.3-3 TB/s on such runs against ~4.5 on
+// >= 128-B runs (tools/scatter_probe.hip).  Two stable passes over the two
+// digits of rank = c * F + f (F = 2^fbits fine buckets, C = ceil(nranks / F)
+// coarse ones, F, C ~ sqrt(nranks)) write runs of ~4096 / F and ~4096 / C
+// keys, at the price of an intermediate array (key row + original index):
+//   pass 1 (k_bucket_pass1): per counting tile, the tile's keys in fine-bucket
+//          order into the intermediate at fbase[f] + (fine-f keys of earlier
+//          tiles), stable: the intermediate is ordered by (f, original index);
+//   pass 2 (k_bucket_pass2): per segment = (f, SG consecutive chunks of
+//          kBucketChunk tiles), a contiguous stretch of the intermediate that
+//          holds, in original order, the fine-f keys of those tiles.  Sorted
+//          by c in sub-tiles of 4096 keys, each key goes to its final slot:
+//          bucket r = c * F + f receives the segment's keys at base[r] +
+//          chunks[g0][r] onwards, in order.
+// Both passes take their positions from the single pass's per-tile counts
+// (count kernel + scans): no extra counting and no inter-workgroup waits.
+constexpr u32 kTpMaxDigits = 128;  // F, C <= 128: nranks <= 8192 = 2^13 -> F = 2^7, C = 2^6
+struct TwoPass {
+  u32 fbits, F, C, cbits;
+  const u64 *fbase;   // [F] first intermediate row of fine bucket f
+  const u64 *totals;  // [nranks] keys per rank
+  uint8_t *ikeys;     // [n][L] intermediate key rows
+  u32 *iidx;          // [n] intermediate original indices
+  u64 nchunks, SG, nsegf, nseg;  // chunks of counting tiles; chunks per segment; segments per f; total
+};
+
+// Digit-run tables and scan of a tile sorted by a digit < ND <= kB (one thread
+// per digit): on return run[w][d] = tile-local start of wave w's keys of
+// digit d, and delta[d] = dst(d, tile-local start of d) - that start, i.e.
+// the global slot of the tile's first digit-d key minus its local slot.
+template <int W, class Dst>
+__device__ __forceinline__ void digit_starts(const RunTab<false> &run, u32 ND, u32 *delta, u32 *tcount,
+                                             u32 *scan_scratch, const Dst &dst) {
+  const u32 d = threadIdx.x;
+  u32 s = 0;
+  if (d < ND)
 #pragma unroll
-      for (int jj = 0; jj < kPer; ++jj) {
-        const u32 j = min(jj * kB + threadIdx.x, tn - 1);
-        hv[jj] = stage[j];
-        gp[jj] = delta[(u32)rk.mod(hv[jj])] + j;
-        if (jj * kB + threadIdx.x < tn) out.head(gp[jj], tbase + sidx[j]);
-      }
+    for (int w = 0; w < W; ++w) s += run.get(w, d);
+  u32 acc = block_exclusive_scan<W>(s, scan_scratch);
+  if (d < ND) {
+    delta[d] = dst(d) - acc;
+    if (tcount) tcount[d] = s;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const u32 v = run.get(w, d);
+      run.set(w, d, acc);
+      acc += v;
+    }
+  }
+}
+
+// Pass-1 units are the counting tiles (kTpCountTile keys); both passes work
+// through their units in sub-tiles of W x KPL x 64 keys, carrying each
+// digit's next slot across sub-tiles.  Runs stay long with small sub-tiles
+// (1024 keys over 32 digits: 32-key runs), and small sub-tiles keep LDS and
+// VGPRs per workgroup low, so that several workgroups per CU overlap one
+// another's load / rank / store phases.
+constexpr u32 kTpCountTile = 4096;
+constexpr int kTpW = 4, kTpKPL = 8, kTpPerCu = 4;
+template <int W, int KPL>
+constexpr size_t pass1_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 2 + 1); }
+template <int W, int KPL>
+constexpr size_t pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
+
+// DBG (tuning build only, timing-only, wrong results): 1 = every sub-tile
+// stored contiguously at its own position, as if all runs were one.
+template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, TileStarts ts, u64 ntiles,
+                    TwoPass tp) {
+  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
+  static_assert(kTpCountTile % kTile == 0, "sub-tiles of a counting tile");
+  extern __shared__ u64 lds64[];
+  u64 *stage = lds64;                                            // [kTile] key pieces
+  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile] sub-tile-local index
+  uint8_t *sdig = reinterpret_cast<uint8_t *>(sidx + kTile);     // [kTile] fine digit
+  __shared__ u32 runt[W * kTpMaxDigits];
+  __shared__ u32 running[kTpMaxDigits];  // next intermediate row of fine bucket f
+  __shared__ u32 delta[kTpMaxDigits];
+  __shared__ u32 tcount[kTpMaxDigits];
+  __shared__ u32 scan_scratch[W];
+  const RunTab<false> run{runt, tp.F};
+  const u32 fmask = tp.F - 1;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u32 q0 = wave * kSub + lane;
+  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
+    const u64 t = o.t;
+    const u64 tbase = t * kTpCountTile;
+    const u32 ttn = (u32)min((u64)kTpCountTile, n - tbase);
+    // the tile's rows in fine bucket f follow those of the earlier tiles:
+    // fbase[f] + the earlier keys of the ranks r = c*F + f
+    if (threadIdx.x < tp.F) running[threadIdx.x] = (u32)tp.fbase[threadIdx.x];
+    __syncthreads();
+    const u64 crow = (t / kBucketChunk) * nranks, trow = t * nranks;
+    for (u32 r = threadIdx.x; r < nranks; r += kB)
+      atomicAdd(&running[r & fmask], ts.chunks[crow + r] + ts.counts[trow + r]);
+    for (u32 s0 = 0; s0 < ttn; s0 += kTile) {
+      const u32 tn = min(kTile, ttn - s0);
+      const u64 sbase = tbase + s0;
+      for (u32 j = threadIdx.x; j < W * tp.F; j += kB) runt[j] = 0;
+      RegReader<L / 4> kr[KPL];
+#pragma unroll
+      for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(sbase + q0 + g * 64, n - 1), kr[g]);
+      u32 ff[KPL];
+#pragma unroll
+      for (int g = 0; g < KPL; ++g) ff[g] = (u32)rk.mod(city64(kr[g], (u64)L)) & fmask;
       __syncthreads();
 #pragma unroll
       for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+        if (q0 + g * 64 < tn) run.add(wave, ff[g], 1u);
       __syncthreads();
+      digit_starts<W>(run, tp.F, delta, tcount, scan_scratch, [&](u32 f) { return running[f]; });
+      __syncthreads();
+      u32 lp[KPL];
+      rank_groups<KPL>(run, wave, ff, q0, tn, tp.fbits, lp);
 #pragma unroll
-      for (int jj = 0; jj < kPer; ++jj) {
+      for (int g = 0; g < KPL; ++g)
+        if (q0 + g * 64 < tn) {
+          stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+          sidx[lp[g]] = (uint16_t)(q0 + g * 64);
+          sdig[lp[g]] = (uint8_t)ff[g];
+        }
+      __syncthreads();
+      u32 gp[KPL];
+#pragma unroll
+      for (int jj = 0; jj < KPL; ++jj) {
         const u32 j = jj * kB + threadIdx.x;
-        if (j < tn) out.tail8(gp[jj], hv[jj], stage[j]);
+        if (j < tn) {
+          gp[jj] = (DBG ? (u32)sbase : delta[sdig[j]]) + j;
+          tp.iidx[gp[jj]] = (u32)(sbase + sidx[j]);
+          *reinterpret_cast<u64 *>(tp.ikeys + (u64)gp[jj] * L) = stage[j];
+        }
       }
-      __syncthreads();
-      continue;
-    }
 #pragma unroll
-    for (int jj = 0; jj < kPer; ++jj) {
-      const u32 j = jj * kB + threadIdx.x;
-      if (j < tn) {
-        const u64 hv = stage[j];
-        gp[jj] = delta[(u32)rk.mod(hv)] + j;
-        out.meta(gp[jj], hv, tbase + sidx[j]);
-      }
-    }
-    if (out.has_keys()) {
-#pragma unroll
-      for (int c = 0; c < L / 8; ++c) {
+      for (int c = 1; c < L / 8; ++c) {
         __syncthreads();
 #pragma unroll
         for (int g = 0; g < KPL; ++g)
           if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
         __syncthreads();
 #pragma unroll
-        for (int jj = 0; jj < kPer; ++jj) {
+        for (int jj = 0; jj < KPL; ++jj) {
           const u32 j = jj * kB + threadIdx.x;
-          if (j < tn) out.key8(gp[jj], c, stage[j]);
+          if (j < tn) *reinterpret_cast<u64 *>(tp.ikeys + (u64)gp[jj] * L + 8 * c) = stage[j];
         }
       }
+      __syncthreads();
+      if (threadIdx.x < tp.F) running[threadIdx.x] += tcount[threadIdx.x];
+    }
+    __syncthreads();
+  }
+}
+
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_bucket_pass2(FastMod rk, u32 nranks, TileStarts ts, TwoPass tp, Out out) {
+  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
+  extern __shared__ u64 lds64[];
+  u64 *stage = lds64;                                    // [kTile] digests, then key pieces
+  u32 *sidx = reinterpret_cast<u32 *>(stage + kTile);  // [kTile] original index
+  __shared__ u32 runt[W * kTpMaxDigits];
+  __shared__ u32 running[kTpMaxDigits];  // next final slot of bucket c*F + f
+  __shared__ u32 delta[kTpMaxDigits];
+  __shared__ u32 tcount[kTpMaxDigits];
+  __shared__ u32 seg[2];  // rows of the segment before it in fine bucket f; its length
+  __shared__ u32 scan_scratch[W];
+  const RunTab<false> run{runt, tp.C};
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u32 q0 = wave * kSub + lane;
+  const u32 fbits = tp.fbits;
+  auto coarse = [&](u64 h) { return (u32)rk.mod(h) >> fbits; };
+  for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
+    const u32 f = (u32)(o.t / tp.nsegf);
+    const u64 g0 = (o.t % tp.nsegf) * tp.SG;
+    const u64 g1 = min(g0 + tp.SG, tp.nchunks);
+    if (threadIdx.x < 2) seg[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x < tp.C) {
+      const u32 r = threadIdx.x * tp.F + f;
+      u32 lo = 0, cnt = 0;
+      if (r < nranks) {
+        lo = ts.chunks[g0 * nranks + r];
+        cnt = (u32)((g1 < tp.nchunks ? (u64)ts.chunks[g1 * nranks + r] : tp.totals[r]) - lo);
+        running[threadIdx.x] = (u32)ts.base[r] + lo;
+      }
+      atomicAdd(&seg[0], lo);
+      atomicAdd(&seg[1], cnt);
+    }
+    __syncthreads();
+    const u32 sstart = (u32)tp.fbase[f] + seg[0], slen = seg[1];
+    for (u32 k0 = 0; k0 < slen; k0 += kTile) {
+      const u32 tn = min(kTile, slen - k0);
+      const u64 p0 = (u64)sstart + k0;
+      for (u32 j = threadIdx.x; j < W * tp.C; j += kB) runt[j] = 0;
+      RegReader<L / 4> kr[KPL];
+      u32 ix[KPL];
+#pragma unroll
+      for (int g = 0; g < KPL; ++g) {
+        const u64 p = p0 + min(q0 + g * 64, tn - 1);
+        load_key_regs<L, true>(tp.ikeys, p, kr[g]);
+        ix[g] = __builtin_nontemporal_load(tp.iidx + p);
+      }
+      u64 h[KPL];
+      u32 cc[KPL];
+#pragma unroll
+      for (int g = 0; g < KPL; ++g) {
+        h[g] = city64(kr[g], (u64)L);
+        cc[g] = coarse(h[g]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < KPL; ++g)
+        if (q0 + g * 64 < tn) run.add(wave, cc[g], 1u);
+      __syncthreads();
+      digit_starts<W>(run, tp.C, delta, tcount, scan_scratch, [&](u32 c) { return running[c]; });
+      __syncthreads();
+      u32 lp[KPL];
+      rank_groups<KPL>(run, wave, cc, q0, tn, tp.cbits, lp);
+#pragma unroll
+      for (int g = 0; g < KPL; ++g)
+        if (q0 + g * 64 < tn) {
+          stage[lp[g]] = h[g];
+          sidx[lp[g]] = ix[g];
+        }
+      __syncthreads();
+      if constexpr (DBG) {
+        __shared__ u32 dbase[1];
+        if (threadIdx.x == 0) dbase[0] = (u32)p0;
+        __syncthreads();
+        staged_store<L, KPL, kB>(stage, dbase, tn, kr, lp, q0, [](u64) { return 0u; },
+                                 [&](u32 j) { return (u64)sidx[j]; }, out);
+      } else {
+        staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
+      }
+      __syncthreads();
+      if (threadIdx.x < tp.C) running[threadIdx.x] += tcount[threadIdx.x];
     }
     __syncthreads();
   }

@@ -923,12 +923,16 @@ PDHT_API int pdht_hip_mixed_lengths_dev(uint64_t seed, uint64_t first, size_t n,
 namespace pdht {
 struct BucketWs {
   u32 *counts, *chunks;
-  u64 *totals, *base;
+  u64 *totals, *base, *fbase;
+  uint8_t *ikeys;  // two-pass intermediate (8/16/32-B keys): [n][keysize] key rows
+  u32 *iidx;       //   and [n] original indices
   size_t bytes;
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
-// Sized for the smallest tile any scatter kernel uses.
-static BucketWs bucket_layout(void *ws, size_t n, u32 nranks) {
+static bool two_pass_keysize(size_t keysize) { return keysize == 8 || keysize == 16 || keysize == 32; }
+// Sized for the smallest tile any scatter kernel uses, plus the two-pass
+// intermediate for the key sizes that can take that path.
+static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
   const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   BucketWs w{};
@@ -942,6 +946,14 @@ static BucketWs bucket_layout(void *ws, size_t n, u32 nranks) {
   off += round256((size_t)nranks * 8);
   w.base = reinterpret_cast<u64 *>(p + off);
   off += round256((size_t)nranks * 8);
+  w.fbase = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)kTpMaxDigits * 8);
+  if (two_pass_keysize(keysize)) {
+    w.ikeys = p + off;
+    off += round256(n * keysize);
+    w.iidx = reinterpret_cast<u32 *>(p + off);
+    off += round256(n * 4);
+  }
   w.bytes = off;
   return w;
 }
@@ -961,23 +973,24 @@ struct BucketArgs {
   u64 ntiles;
 };
 
-template <int L, class Out, bool PACK = false>
+template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL>
 static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
   static const char *const pnames[3] = {"k_bucket_scatter_staged<8B,u16>", "k_bucket_scatter_staged<16B,u16>",
                                         "k_bucket_scatter_staged<32B,u16>"};
   g_kernel = (PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
-  const size_t bytes = staged_lds_bytes(a.nranks, kStW, kStKPL, PACK);
-  auto fn = &k_bucket_scatter_staged<L, Out, kStW, kStKPL, PACK>;
+  const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK);
+  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
   const int per_cu = bytes <= 53 * 1024 ? 3 : bytes <= 80 * 1024 ? 2 : 1;
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-  fn<<<g, kStW * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+  fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
   return 0;
 }
 
+#ifdef PDHT_HIP_TUNING
 template <int W, int L, int KPL, class Out>
 static int launch_reg(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_scatter_reg<8B>", "k_bucket_scatter_reg<16B>",
@@ -989,6 +1002,8 @@ static int launch_reg(const BucketArgs &a, const Out &out, hipStream_t st, int d
       a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
   return 0;
 }
+
+#endif
 
 template <int W, class Out>
 static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st, int dev) {
@@ -1020,7 +1035,50 @@ static int launch_gather(const BucketArgs &a, const Out &out, u32 L, int lk, hip
 }
 #endif
 
-enum class BucketKernel { kGather, kStaged, kReg, kGeneric };
+// Two-pass bucketing from this many ranks up (interleaved
+// A/B on 16M keys; at 1024 ranks one pass is 10 % faster for 8-B keys, equal
+// for 16-B keys, 30 % faster for 32-B keys; at 2048 ranks two passes are 1.3x
+// faster for 8-B keys and at 8192 ranks 2.1x).
+static u32 two_pass_min_ranks(size_t keysize) { return keysize == 8 ? 1536 : keysize == 16 ? 1025 : 2049; }
+
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0>
+static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
+  static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
+  constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;  // waves per SIMD
+  const size_t b1 = pass1_lds_bytes<W, KPL>(), b2 = pass2_lds_bytes<W, KPL>();
+  auto f1 = &k_bucket_pass1<L, W, KPL, WPE, DBG>;
+  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG>;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
+  const u64 cus = (u64)std::max(1, g_dev[dev].cus);
+  unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU);
+  if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
+  f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, a.nranks, a.ts, a.ntiles, tp);
+  unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
+  if (g2 >= 8) g2 &= ~7u;
+  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, a.ts, tp, out);
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  return 0;
+}
+
+template <int L, class Out>
+static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
+#ifdef PDHT_HIP_TUNING
+  // 73-76: sub-tile shape (waves x keys per lane) and workgroups per CU;
+  // 77: 73 with contiguous stores (timing-only, wrong results)
+  switch (tuning_variant()) {
+    case 73: return launch_two_pass<L, Out, 4, 8, 4>(a, tp, out, st, dev);
+    case 74: return launch_two_pass<L, Out, 8, 4, 4>(a, tp, out, st, dev);
+    case 75: return launch_two_pass<L, Out, 4, 16, 2>(a, tp, out, st, dev);
+    case 76: return launch_two_pass<L, Out, 4, 4, 6>(a, tp, out, st, dev);
+    case 77: return launch_two_pass<L, Out, 4, 8, 4, 1>(a, tp, out, st, dev);  // timing-only
+    default: break;
+  }
+#endif
+  return launch_two_pass<L, Out>(a, tp, out, st, dev);
+}
+
+enum class BucketKernel { kGather, kStaged, kReg, kGeneric, kTwoPass };
 
 // Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
 // (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
@@ -1035,7 +1093,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   if (n >= (1ull << 32)) return fail("bucketing: n must be < 2^32 per call%s", "");
   if (!bucket_offsets) return fail("bucket_offsets must not be NULL%s", "");
   if (n && (!keys || keysize == 0)) return fail("null keys or zero keysize%s", "");
-  const BucketWs w = bucket_layout(workspace, n, nranks);
+  const BucketWs w = bucket_layout(workspace, n, keysize, nranks);
   if (!workspace || workspace_bytes < w.bytes) return fail("workspace too small%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
@@ -1043,9 +1101,11 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   // 2048 ranks, register scatter above; other lengths -> generic.
   const uintptr_t al = (uintptr_t)keys | out_al;
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
-  BucketKernel kind = !fixed                     ? BucketKernel::kGeneric
-                      : nranks > kStagedMaxRanks ? BucketKernel::kReg
-                                                 : BucketKernel::kStaged;
+  // (two_pass_min_ranks <= kStagedMaxRanks + 1: the staged scatter covers
+  // every nranks below the two-pass threshold)
+  BucketKernel kind = !fixed                                ? BucketKernel::kGeneric
+                      : nranks >= two_pass_min_ranks(keysize) ? BucketKernel::kTwoPass
+                                                              : BucketKernel::kStaged;
   int ga_w = kGaW, ga_kpl = kGaKPL;
 #ifdef PDHT_HIP_TUNING
   // 21 generic, 22 register scatter; 54 the gather scatter (16384-key tiles,
@@ -1053,6 +1113,11 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   // tiles (4 waves x 32 / 8 waves x 16 keys per lane); 55-57 its timing-only
   // builds; 58 producer/consumer scatter; 50 staged with u16 run tables.
   // All measured slower than the staged scatter.
+  // 70: one pass (staged / register scatter) at any nranks; 71: two passes
+  // at any nranks >= 2.
+  if (tuning_variant() == 70 && kind == BucketKernel::kTwoPass)
+    kind = nranks > kStagedMaxRanks ? BucketKernel::kReg : BucketKernel::kStaged;
+  if (tuning_variant() == 71 && fixed && nranks >= 2) kind = BucketKernel::kTwoPass;
   if (tuning_variant() == 21) kind = BucketKernel::kGeneric;
   if (tuning_variant() == 22 && fixed) kind = BucketKernel::kReg;
   if (tuning_variant() >= 52 && tuning_variant() <= 58 && nranks <= kStagedMaxRanks) kind = BucketKernel::kGather;
@@ -1061,8 +1126,9 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
 #endif
   const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
   const int reg_kpl = keysize == 32 ? 8 : 16;
-  const u64 tile = kind == BucketKernel::kGather   ? (u64)ga_w * ga_kpl * 64
-                   : kind == BucketKernel::kStaged ? kStTile
+  const u64 tile = kind == BucketKernel::kGather     ? (u64)ga_w * ga_kpl * 64
+                   : kind == BucketKernel::kTwoPass ? kTpCountTile
+                   : kind == BucketKernel::kStaged   ? kStTile
                    : kind == BucketKernel::kReg    ? (u64)waves * reg_kpl * 64
                                                    : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
@@ -1094,12 +1160,28 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   } else {
     HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
   }
-  k_bucket_base<<<1, kBlock, 0, st>>>(w.totals, nranks, w.base, bucket_offsets);
+  TwoPass tp{};
+  if (kind == BucketKernel::kTwoPass) {
+    tp.fbits = (a.nbits + 1) / 2;
+    tp.F = 1u << tp.fbits;
+    tp.C = (nranks + tp.F - 1) >> tp.fbits;
+    tp.cbits = a.nbits - tp.fbits;
+    tp.fbase = w.fbase;
+    tp.totals = w.totals;
+    tp.ikeys = w.ikeys;
+    tp.iidx = w.iidx;
+    tp.nchunks = nchunks;
+    tp.SG = std::max<u64>(1, tp.F / 32);  // ~4096 keys per segment
+    tp.nsegf = (nchunks + tp.SG - 1) / tp.SG;
+    tp.nseg = (u64)tp.F * tp.nsegf;
+  }
+  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, tp.fbits,
+                                      kind == BucketKernel::kTwoPass ? w.fbase : nullptr);
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
-    const int lk = fixed ? (int)keysize : 0;
 #ifdef PDHT_HIP_TUNING
+    const int lk = fixed ? (int)keysize : 0;
     if (kind == BucketKernel::kGather && !(tuning_variant() >= 55 && tuning_variant() <= 58 && lk == 8)) {
       if (ga_w == 8 && ga_kpl == 32)
         rc = launch_gather<8, 32>(a, out, (u32)keysize, lk, st, dev);
@@ -1134,15 +1216,21 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
                            : launch_staged<32, Out, true>(a, out, st, dev);
     else
 #endif
-    if (kind == BucketKernel::kStaged)
+    if (kind == BucketKernel::kTwoPass)
+      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev)
+           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev)
+                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev);
+    else if (kind == BucketKernel::kStaged)
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
                            : launch_staged<32, Out>(a, out, st, dev);
+#ifdef PDHT_HIP_TUNING
     else if (kind == BucketKernel::kReg)
       rc = keysize == 8 ? (waves == 8 ? launch_reg<8, 8, 16>(a, out, st, dev) : launch_reg<4, 8, 16>(a, out, st, dev))
            : keysize == 16
                ? (waves == 8 ? launch_reg<8, 16, 16>(a, out, st, dev) : launch_reg<4, 16, 16>(a, out, st, dev))
                : (waves == 8 ? launch_reg<8, 32, 8>(a, out, st, dev) : launch_reg<4, 32, 8>(a, out, st, dev));
+#endif
     else
       rc = waves == 8 ? launch_wg<8>(a, out, (u32)keysize, st, dev) : launch_wg<4>(a, out, (u32)keysize, st, dev);
     if (rc) return rc;
@@ -1152,8 +1240,8 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
 }
 }  // namespace pdht
 
-PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, uint32_t nranks) {
-  return bucket_layout(nullptr, n, nranks).bytes;
+PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks) {
+  return bucket_layout(nullptr, n, keysize, nranks).bytes;
 }
 
 PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,

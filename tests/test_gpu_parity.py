@@ -427,13 +427,17 @@ BUCKET_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in 
                  for n in (4095, 300007)]
 BUCKET_CASES += [(L, nr, n, v) for v in (54, 58) for L in (8, 13, 16) for nr in (7, 1000, 2048)
                  for n in (1, 16383, 16385, 1 << 20)]
+BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2049, 8192)
+                 for n in (1, 4095, 300007, (1 << 20) + 5)]
 
 
 def _bucket_kernel(L, nranks, variant):
     """Product: the staged scatter for 8/16/32-B keys up to 2048 ranks, the
     register scatter above, the generic one for other lengths.  Tuning
     variants: 21 forces the generic-length kernel, 22 the register one, 54 the
-    gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys)."""
+    gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys),
+    70 one pass at any nranks, 71 two passes from 2 ranks up.  The product
+    sorts 8/16/32-B keys in two passes from 1536 / 1025 / 2049 ranks."""
     wg = "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
     if variant == 21:
         return wg
@@ -444,6 +448,9 @@ def _bucket_kernel(L, nranks, variant):
     if variant in (54, 58) and nranks <= 2048:
         return f"k_bucket_scatter_gather<{L}B>" if L in (8, 16, 32) else "k_bucket_scatter_gather<any>"
     if L in (8, 16, 32):
+        two_pass_from = {8: 1536, 16: 1025, 32: 2049}[L]
+        if (variant == 71 and nranks >= 2) or (variant != 70 and nranks >= two_pass_from):
+            return f"k_bucket_pass2<{L}B>"
         return f"k_bucket_scatter_{'staged' if nranks <= 2048 else 'reg'}<{L}B>"
     return wg
 
@@ -463,6 +470,27 @@ def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     assert (ix.cpu().numpy().view(np.uint32) == order).all()
     assert (u64(mb) == m2[order]).all()
     assert (pt.cpu().numpy().view(np.uint32) == p2[order]).all()
+    assert (ko.cpu().numpy() == k[order]).all()
+    want_offs = np.concatenate([[0], np.cumsum(np.bincount(r2, minlength=nranks))])
+    assert (offs.cpu().numpy() == want_offs).all()
+
+
+@pytest.mark.parametrize("L,nranks,variant", [(L, nr, v) for L in (8, 16, 32) for nr in (1000, 8192)
+                                               for v in (0, 70)])
+def test_bucket_skewed(dev, oracle, L, nranks, variant):
+    """Few distinct keys: whole batches land in a handful of buckets, so the
+    two-pass sort meets segments far longer than its 4096-key sub-tiles and
+    tiles whose keys all share one bucket."""
+    rng = np.random.default_rng(L + nranks)
+    distinct = rng.integers(0, 256, (3, L), dtype=np.uint8)
+    k = distinct[rng.integers(0, 3, 700_001)]
+    with P.tuning(variant) if variant else _nullctx():
+        ko, mb, pt, ix, offs = P.bucket_batch(to_dev(k, dev), 3, nranks)
+        assert P.last_kernel() == _bucket_kernel(L, nranks, variant)
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, nranks)
+    order = np.argsort(r2, kind="stable")
+    assert (ix.cpu().numpy().view(np.uint32) == order).all()
+    assert (u64(mb) == m2[order]).all()
     assert (ko.cpu().numpy() == k[order]).all()
     want_offs = np.concatenate([[0], np.cumsum(np.bincount(r2, minlength=nranks))])
     assert (offs.cpu().numpy() == want_offs).all()
@@ -491,6 +519,8 @@ def test_bucket_optional_outputs(dev, oracle, L):
 RECORD_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 7, 1000, 2049, 8192)
                 for n in (0, 1, 4095, 100003)]
 RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 54, 58) for L in (8, 16, 32) for nr in (7, 1000, 2048)
+                 for n in (4097, 300007)]
+RECORD_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (7, 1000, 8192)
                  for n in (4097, 300007)]
 
 
@@ -695,7 +725,7 @@ def test_batches_capture_in_hip_graph(dev, oracle):
     out = torch.empty(n, dtype=torch.int64, device=dev)
     pl = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
           torch.empty(n, dtype=torch.int32, device=dev))
-    ws = torch.empty(P.bucket_workspace_bytes(n, 1000), dtype=torch.uint8, device=dev)
+    ws = torch.empty(P.bucket_workspace_bytes(n, 8, 1000), dtype=torch.uint8, device=dev)
     bk = P.bucket_batch(k8, 3, 1000, workspace=ws)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())

@@ -31,6 +31,19 @@ M = 1 << 20
 
 def workload(name, dev):
     """(step(), result-for-equality(), algorithmic bytes per step)"""
+    if name.startswith(("bucket_", "records_")):  # bucket_<L>_<nranks>, records_<L>_<nranks>
+        kind, L, nr = name.split("_")
+        L, nr, n = int(L), int(nr), 16 * M
+        keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
+        ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
+        if kind == "records":
+            outs = P.bucket_records(keys, nr, workspace=ws)
+            return ((lambda: P.bucket_records(keys, nr, out=outs, workspace=ws)),
+                    (lambda: torch.cat([outs[0].view(-1)[:1 << 20].long(), outs[1]])),
+                    n * (L + P.bucket_record_bytes(L)))
+        outs = P.bucket_batch(keys, 3, nr, workspace=ws)
+        return ((lambda: P.bucket_batch(keys, 3, nr, out=outs, workspace=ws)),
+                (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (L + L + 8 + 4 + 4))
     if name in ("cfg2", "cfg4", "long", "long64", "place", "bucket"):
         L = {"cfg2": 64, "cfg4": 64, "long": 1024, "long64": 1024, "place": 8, "bucket": 8}[name]
         n = M if name in ("long", "long64") else 16 * M
@@ -46,7 +59,7 @@ def workload(name, dev):
             outs = P.place_batch(keys, 3, 1024)
             return ((lambda: P.place_batch(keys, 3, 1024, hist=hist, out=outs)),
                     (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 24)
-        ws = torch.empty(P.bucket_workspace_bytes(n, 1024), dtype=torch.uint8, device=dev)
+        ws = torch.empty(P.bucket_workspace_bytes(n, 8, 1024), dtype=torch.uint8, device=dev)
         outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
         return ((lambda: P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)),
                 (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (8 + 8 + 8 + 4 + 4))
