@@ -138,24 +138,46 @@ __global__ __launch_bounds__(64) void k_bucket_colscan(u32 *__restrict__ counts,
   chunks[(u64)blockIdx.y * nranks + r] = run;
 }
 
-// Thread = rank: exclusive scan over the chunk sums (in place) and the total.
-__global__ __launch_bounds__(kBlock) void k_bucket_chunkscan(u32 *__restrict__ chunks, u64 nchunks,
-                                                             u32 nranks, u64 *__restrict__ totals) {
-  const u32 r = blockIdx.x * kBlock + threadIdx.x;
-  if (r >= nranks) return;
+// Exclusive scan over the chunk sums (in place) and the per-rank totals.
+// Workgroup = 64 ranks (lane = rank) x kCsWaves waves; wave w scans its own
+// contiguous share of the chunks, loading up to 16 rows before it stores any
+// (a load wait also waits for older stores), then adds the sums of the waves
+// before it: one or two memory round trips instead of nchunks / 16.
+constexpr int kCsWaves = 16;
+__global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan(u32 *__restrict__ chunks, u64 nchunks,
+                                                                    u32 nranks, u64 *__restrict__ totals) {
+  __shared__ u32 wsum[kCsWaves][64];
+  const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const u32 r = blockIdx.x * 64 + lane;
+  const u64 per = (nchunks + kCsWaves - 1) / kCsWaves;
+  const u64 c0 = min((u64)wave * per, nchunks), c1 = min(c0 + per, nchunks);
   constexpr u32 B = 16;
-  u64 run = 0;
-  for (u64 c0 = 0; c0 < nchunks; c0 += B) {
-    u32 v[B];
+  u32 local = 0;  // this wave's chunk sum
+  if (r < nranks)
+    for (u64 c = c0; c < c1; c += B) {
+      u32 v[B];
 #pragma unroll
-    for (u32 j = 0; j < B; ++j) v[j] = c0 + j < nchunks ? chunks[(c0 + j) * nranks + r] : 0;
+      for (u32 j = 0; j < B; ++j) v[j] = c + j < c1 ? chunks[(c + j) * nranks + r] : 0;
 #pragma unroll
-    for (u32 j = 0; j < B; ++j) {
-      if (c0 + j < nchunks) chunks[(c0 + j) * nranks + r] = (u32)run;
-      run += v[j];
+      for (u32 j = 0; j < B; ++j) local += v[j];
     }
+  wsum[wave][lane] = local;
+  __syncthreads();
+  u64 run = 0;
+  for (u32 w = 0; w < wave; ++w) run += wsum[w][lane];
+  if (r < nranks) {
+    for (u64 c = c0; c < c1; c += B) {
+      u32 v[B];
+#pragma unroll
+      for (u32 j = 0; j < B; ++j) v[j] = c + j < c1 ? chunks[(c + j) * nranks + r] : 0;
+#pragma unroll
+      for (u32 j = 0; j < B; ++j) {
+        if (c + j < c1) chunks[(c + j) * nranks + r] = (u32)run;
+        run += v[j];
+      }
+    }
+    if (wave == kCsWaves - 1) totals[r] = run;
   }
-  totals[r] = run;
 }
 
 // ------------------------------------------------------------- helpers ---

@@ -1155,7 +1155,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
                                                    tile);
     k_bucket_colscan<<<dim3((nranks + 63) / 64, (unsigned)nchunks), 64, 0, st>>>(w.counts, ntiles, nranks,
                                                                                  w.chunks);
-    k_bucket_chunkscan<<<(nranks + kBlock - 1) / kBlock, kBlock, 0, st>>>(w.chunks, nchunks, nranks,
+    k_bucket_chunkscan<<<(nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunks, nchunks, nranks,
                                                                         w.totals);
   } else {
     HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
