@@ -447,9 +447,10 @@ __device__ __forceinline__ u32 xpose_slot(u32 k, u32 c) { return 4 * k + (c ^ ((
 // 4 contiguous 16-B pieces of the NEXT tile (global_load_dwordx4, 1 KiB per
 // wave-instruction) while the current tile hashes, then writes them into the
 // image with ds_write_b128.
-template <class Algo, class Sink, bool LNT = false, int DEPTH = 1>
-__global__ __launch_bounds__(kBlock) void k_fixed_xpose64(const uint8_t *__restrict__ keys, u64 n,
-                                                          Algo algo, Sink sink) {
+template <class Algo, class Sink, bool LNT = false, int DEPTH = 1, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_fixed_xpose64(const uint8_t *__restrict__ keys, u64 n,
+                                                         Algo algo, Sink sink) {
+  constexpr int kWavesPerBlock = BLOCK / 64;
   __shared__ __attribute__((aligned(16))) u32x4 img[kWavesPerBlock][256];  // 4 KiB per wave
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;

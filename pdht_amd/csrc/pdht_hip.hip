@@ -141,6 +141,12 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
   }
 }
 
+template <class Sink>
+static bool sink_has_hist(const Sink &s) {
+  if constexpr (std::is_same<Sink, SinkPlace>::value) return s.hist != nullptr;
+  return false;
+}
+
 // Fixed-length keys: the register-direct / LDS-transposed kernels for the
 // specialised lengths when the layout allows them, else the window kernel
 // (a 64-key tile fits 12 or 16 KiB of LDS), else per-lane global reads.
@@ -171,6 +177,21 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
         HIP_TRY(hipGetLastError());
         return 0;
       }
+      if (tuning_variant() == 80 || tuning_variant() == 81) {  // 1024-thread workgroups, 1 / 2 per CU
+        g_kernel = tuning_variant() == 80 ? "k_fixed_xpose64<nt,d2,1024>@1" : "k_fixed_xpose64<nt,d2,1024>@2";
+        k_fixed_xpose64<Algo, SinkNt, true, 2, 1024>
+            <<<grid_for((n + 1023) / 1024, tuning_variant() == 80 ? 1 : 2, dev), 1024, 0, st>>>(k, n, algo,
+                                                                                                sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+      if (tuning_variant() == 82) {  // the 256-thread shape whatever the histogram
+        g_kernel = "k_fixed_xpose64<nt,d2>@3";
+        k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
       if (tuning_variant() == 26) {  // plain digest stores (r01: 2-6 % slower)
         g_kernel = "k_fixed_xpose64<nt-load,plain-store,d2>@3";
         k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
@@ -181,7 +202,22 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
     }
 #endif
     // measured fastest (tools/kbench.py): non-temporal loads
-    // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU
+    // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU.
+    // Placement with a histogram on up to 4M keys: 1024-thread workgroups, 1
+    // per CU -- every workgroup ends with one device-scope atomic per bin, and
+    // with few ranks those all hit one cache line: 768 flushing workgroups
+    // cost ~6 us of a 24-us launch on 1M keys (cfg1), 256 cost ~1 us
+    // (tools/abbench.py cfg1: 24.3 -> 18.3 us); on 16M keys the wide shape
+    // streams 3-5 % slower and the 256-thread one stays.
+    if constexpr (kShort) {
+      if (sink_has_hist(sink) && n <= (4u << 20)) {
+        g_kernel = "k_fixed_xpose64<nt,d2,1024>@1";
+        k_fixed_xpose64<Algo, SinkNt, true, 2, 1024><<<grid_for((n + 1023) / 1024, 1, dev), 1024, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+    }
     g_kernel = "k_fixed_xpose64<nt,d2>@3";
     if constexpr (kShort)
       k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(

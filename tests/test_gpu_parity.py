@@ -372,10 +372,30 @@ def test_place_hist_many_workgroups(dev, oracle, L):
     P.place_batch(kd, 3, 1000, hist=hist)
     if L in (8, 16):
         assert P.last_kernel().endswith(",1024>@2")
+    else:  # 64-B keys, <= 4M of them, with a histogram: the 1024-thread transpose
+        assert P.last_kernel() == "k_fixed_xpose64<nt,d2,1024>@1"
     P.place_batch(kd[:12345], 3, 1000, hist=hist)
     _, _, r2 = oracle.pdht_hash_fixed(k, 3, 1000)
     want = 5 + np.bincount(r2, minlength=1000) + np.bincount(r2[:12345], minlength=1000)
     assert (hist.cpu().numpy() == want).all()
+
+
+def test_place_hist_64B_large_batch(dev, oracle):
+    """Above 4M 64-B keys the histogram placement streams on the 256-thread
+    transpose (3 per CU); few ranks, so every workgroup's flush hits one line."""
+    n = (4 << 20) + 4097
+    words = P.splitmix64_fill(0x1234, 0, n * 8, device=dev)
+    kd = words.view(torch.uint8).view(n, 64)
+    hist = torch.zeros(4, dtype=torch.int64, device=dev)
+    mb, pt, rk = P.place_batch(kd, 1, 4, hist=hist)
+    assert P.last_kernel() == "k_fixed_xpose64<nt,d2>@3"
+    k = kd[-300000:].cpu().numpy()
+    m2, _, r2 = oracle.pdht_hash_fixed(k, 1, 4)
+    assert (u64(mb[-300000:]) == m2).all()
+    assert (rk[-300000:].cpu().numpy().view(np.uint32) == r2).all()
+    r_all = rk.cpu().numpy().view(np.uint32)
+    assert (hist.cpu().numpy() == np.bincount(r_all, minlength=4)).all()
+    assert (u64(mb) % 4 == r_all).all() and (pt.cpu().numpy() == 0).all()
 
 
 @pytest.mark.parametrize("L", [8, 16, 32])
