@@ -113,10 +113,13 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // workgroups x 1024 bins x 8 B took ~16 us of an 85-us launch; a quarter
     // as many workgroups measured +24 % (8-B keys) and +29 % (16-B keys) on
     // 16M keys, 1024 ranks (tools/placebench.py, r01).
+    // (r02, tools/abbench.py place8_*: 8-B keys stream best at ONE such
+    // workgroup per CU -- 0.80 of the roofline against 0.74 at two, half the
+    // flushes again; 16-B keys stay at two)
     if (sink.hist && keylen == 8) {
-      g_kernel = "k_fixed_direct<8,4,nt-store,1024>@2";
+      g_kernel = "k_fixed_direct<8,4,nt-store,1024>@1";
       k_fixed_direct<8, 4, Algo, SinkNt, false, 1024>
-          <<<grid_for((blocks + 15) / 16, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+          <<<grid_for((blocks + 15) / 16, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
       return;
     }
     if (sink.hist && keylen == 16) {

@@ -44,13 +44,13 @@ def workload(name, dev):
         outs = P.bucket_batch(keys, 3, nr, workspace=ws)
         return ((lambda: P.bucket_batch(keys, 3, nr, out=outs, workspace=ws)),
                 (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (L + L + 8 + 4 + 4))
-    if name.startswith("place64_"):  # place64_<nranks>: 16M x 64 B, nptes 3, + histogram
-        nr, n, L = int(name.split("_")[1]), 16 * M, 64
+    if name.startswith(("place64_", "place16_", "place8_")):  # place<L>_<nranks>: 16M keys, nptes 3, + hist
+        nr, n, L = int(name.split("_")[1]), 16 * M, int(name.split("_")[0][5:])
         keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
         hist = torch.zeros(nr, dtype=torch.int64, device=dev)
         outs = P.place_batch(keys, 3, nr, hist=hist)
         return ((lambda: P.place_batch(keys, 3, nr, hist=hist, out=outs)),
-                (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 80)
+                (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * (L + 16))
     if name in ("cfg1", "cfg1nohist"):  # 1M x 64 B, pdht_hash semantics (nptes 1, 4 ranks) [+ histogram]
         n, L = M, 64
         keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
