@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "exchange", "records",
+                    choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "bucket8k", "exchange", "records",
                              "xrecords", "long"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -131,7 +131,7 @@ def main():
         workload = (f"{cfg}: destination bucketing of {n >> 20}M x 8B keys per GPU by CityHash64 % {nr} into "
                     f"message_t wire records" + (" + all-to-all(v) exchange" if cfg == "xrecords" else ""))
         total_bytes_in = n * L
-    elif cfg in ("bucket", "exchange"):
+    elif cfg in ("bucket", "bucket8k", "exchange"):
         # f4: stable counting sort of 8-B keys by destination rank (keys, mbits,
         # ptindex, original index written at bucketed positions); "exchange"
         # buckets by the world size and ships each bucket to its owner with
@@ -141,10 +141,10 @@ def main():
         sh = D.weak_shard(rank, world, n)
         words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
-        nr = 1024 if cfg == "bucket" else world
+        nr = {"bucket": 1024, "bucket8k": 8192}.get(cfg, world)
         bucketed = {"nranks": nr}
         ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
-        bk = P.bucket_batch(keys, 3, nr, with_ptindex=cfg == "bucket", workspace=ws)
+        bk = P.bucket_batch(keys, 3, nr, with_ptindex=cfg != "exchange", workspace=ws)
 
         def step():
             ko, mb, pt, ix, offs_ = P.bucket_batch(keys, 3, nr, out=bk, workspace=ws)
@@ -152,7 +152,7 @@ def main():
             if cfg == "exchange" and world > 1:
                 bucketed["x"] = D.exchange_buckets(ko, mb, offs_, (ix.long() & 0xFFFFFFFF) + sh.first)
         out = None
-        bytes_per_key = L + L + 8 + 4 + (4 if cfg == "bucket" else 0)
+        bytes_per_key = L + L + 8 + 4 + (4 if cfg != "exchange" else 0)
         workload = (f"{cfg}: destination bucketing of {n >> 20}M x 8B keys per GPU by "
                     f"CityHash64 % {nr}" + (" + all-to-all(v) exchange" if cfg == "exchange" else ""))
         total_bytes_in = n * L
@@ -455,7 +455,7 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
     n = ix.numel()
     msgs, ok = [], True
     folds = golden_folds() or {}
-    g = folds.get("bucket_8B_16M", {})
+    g = folds.get("bucket_8B_16M" if nr == 1024 else f"bucket_8B_16M_{nr}", {})
     r = sh.first // (16 * M)
     if nr == g.get("nranks") and n == g.get("n") and sh.first % n == 0 and r < len(g.get("shards", [])):
         gs = g["shards"][r]
@@ -644,10 +644,10 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
         data, offsets = O.mixed_keys(s_n)
         L = 0
         what = "the first 4M mixed 16..256B keys of the stream (offset-indexed)"
-    elif cfg in ("place", "bucket", "exchange", "records", "xrecords"):
-        s_n, mode, nptes, nranks, L = 4 * M, 2, 3, 1024, 8
+    elif cfg in ("place", "bucket", "bucket8k", "exchange", "records", "xrecords"):
+        s_n, mode, nptes, nranks, L = 4 * M, 2, 3, 8192 if cfg == "bucket8k" else 1024, 8
         data = O.fixed_keys(s_n, 8)
-        what = ("the first 4M x 8B keys, pdht_hash semantics (nptes 3, nranks 1024)"
+        what = (f"the first 4M x 8B keys, pdht_hash semantics (nptes 3, nranks {nranks})"
                 + ("; hashing and placement only, no bucketing" if cfg != "place" else ""))
     else:
         return None

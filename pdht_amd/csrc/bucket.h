@@ -226,11 +226,12 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T *scratch /* NW words */
 // Exclusive scan of the per-rank totals (one workgroup of kBaseThreads, each
 // thread a run of consecutive ranks) -> bucket offsets; with fbase (two-pass
 // bucketing), also the first intermediate row of every fine bucket f = r mod
-// F: the exclusive scan over f of the keys with r mod F == f.
+// F: the exclusive scan of the fine-bucket totals ftot.
 constexpr u32 kBaseThreads = 1024;
 __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restrict__ totals, u32 nranks,
                                                               u64 *__restrict__ base,
                                                               u64 *__restrict__ offsets_out, u32 fbits,
+                                                              const u64 *__restrict__ ftot,
                                                               u64 *__restrict__ fbase) {
   __shared__ u64 scratch[kBaseThreads / 64];
   constexpr u32 kMaxPer = kBucketMaxRanks / kBaseThreads;
@@ -255,9 +256,7 @@ __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restr
   if (nranks == 0 && threadIdx.x == 0) offsets_out[0] = 0;
   if (fbase) {
     const u32 F = 1u << fbits;  // <= kTpMaxDigits
-    u64 fs = 0;
-    if (threadIdx.x < F)
-      for (u32 r = threadIdx.x; r < nranks; r += F) fs += totals[r];
+    const u64 fs = threadIdx.x < F ? ftot[threadIdx.x] : 0;
     __syncthreads();  // scratch reuse
     const u64 fb = block_exclusive_scan<kBaseThreads / 64, u64>(fs, scratch);
     if (threadIdx.x < F) fbase[threadIdx.x] = fb;
@@ -616,15 +615,70 @@ void k_bucket_scatter_staged(
 //          chunks[g0][r] onwards, in order.
 // Both passes take their positions from the single pass's per-tile counts
 // (count kernel + scans): no extra counting and no inter-workgroup waits.
+constexpr u32 kTpCountTile = 4096;  // counting tile = pass-1 unit
 constexpr u32 kTpMaxDigits = 128;  // F, C <= 128: nranks <= 8192 = 2^13 -> F = 2^7, C = 2^6
+constexpr u32 kTpChunkTiles = 8;  // counting tiles per count-chunk (one count workgroup)
 struct TwoPass {
   u32 fbits, F, C, cbits;
-  const u64 *fbase;   // [F] first intermediate row of fine bucket f
-  const u64 *totals;  // [nranks] keys per rank
-  uint8_t *ikeys;     // [n][L] intermediate key rows
-  u32 *iidx;          // [n] intermediate original indices
-  u64 nchunks, SG, nsegf, nseg;  // chunks of counting tiles; chunks per segment; segments per f; total
+  const u32 *countsF;   // [ntiles][F] fine-bucket keys of tile t before it in its 32-tile chunk
+  const u32 *chunksF;   // [ntiles/32][F] ... of the 32-tile chunks before it
+  const u64 *totalsF;   // [F] keys per fine bucket
+  const u32 *chunkcnt;  // [nchunks][nranks] keys of rank r in the count-chunks before chunk g
+  const u64 *base;      // [nranks] first final slot of bucket r
+  const u64 *fbase;     // [F] first intermediate row of fine bucket f
+  uint8_t *ikeys;       // [n][L] intermediate key rows
+  u32 *iidx;            // [n] intermediate original indices
+  u64 ntiles, nchunks;  // counting tiles; count-chunks of kTpChunkTiles tiles
+  u64 SG, nsegf, nseg;  // count-chunks per segment; segments per f; segments
+  // keys of fine bucket f in the tiles before tile t (t <= ntiles)
+  __device__ __forceinline__ u32 fine_before(u64 t, u32 f) const {
+    return t < ntiles ? countsF[t * F + f] + chunksF[(t / kBucketChunk) * F + f] : (u32)totalsF[f];
+  }
 };
+
+// Two-pass counting.  One workgroup per count-chunk of kTpChunkTiles
+// counting tiles: the fine-bucket histogram of every tile -> countsF[t][f],
+// and the rank histogram of the whole chunk -> chunkcnt[g][r].  The single
+// pass's per-tile rank rows are as large as the keys at high rank counts
+// (4096 tiles x 8192 ranks x 4 B = 128 MB for 16M keys, written, scanned and
+// read again); these are nranks/F and kTpChunkTiles times smaller.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__restrict__ keys, u64 n, FastMod rk,
+                                                            u32 nranks, u32 F, u32 *__restrict__ countsF,
+                                                            u32 *__restrict__ chunkcnt, u64 ntiles) {
+  constexpr int U = 128 / L;
+  extern __shared__ u32 hist[];  // [nranks]
+  __shared__ u32 fh[kTpMaxDigits];
+  const u32 fmask = F - 1;
+  const u64 nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
+  for (u64 g = blockIdx.x; g < nchunks; g += gridDim.x) {
+    for (u32 r = threadIdx.x; r < nranks; r += kBlock) hist[r] = 0;
+    const u64 t1 = min((g + 1) * kTpChunkTiles, ntiles);
+    for (u64 t = g * kTpChunkTiles; t < t1; ++t) {
+      if (threadIdx.x < F) fh[threadIdx.x] = 0;
+      __syncthreads();
+      const u64 k0 = t * kTpCountTile;
+      const u64 kend = min(k0 + kTpCountTile, n);
+      for (u64 i = k0 + threadIdx.x; i < kend; i += (u64)kBlock * U) {
+        RegReader<L / 4> kr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_key_regs<L, true>(keys, min(i + u * kBlock, n - 1), kr[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (i + u * kBlock < kend) {
+            const u32 r = (u32)rk.mod(city64(kr[u], (u64)L));
+            atomicAdd(&hist[r], 1u);
+            atomicAdd(&fh[r & fmask], 1u);
+          }
+      }
+      __syncthreads();
+      if (threadIdx.x < F) countsF[t * F + threadIdx.x] = fh[threadIdx.x];
+    }
+    __syncthreads();
+    for (u32 r = threadIdx.x; r < nranks; r += kBlock) chunkcnt[g * nranks + r] = hist[r];
+    __syncthreads();
+  }
+}
 
 // Digit-run tables and scan of a tile sorted by a digit < ND <= kB (one thread
 // per digit): on return run[w][d] = tile-local start of wave w's keys of
@@ -657,7 +711,6 @@ __device__ __forceinline__ void digit_starts(const RunTab<false> &run, u32 ND, u
 // (1024 keys over 32 digits: 32-key runs), and small sub-tiles keep LDS and
 // VGPRs per workgroup low, so that several workgroups per CU overlap one
 // another's load / rank / store phases.
-constexpr u32 kTpCountTile = 4096;
 constexpr int kTpW = 4, kTpKPL = 8, kTpPerCu = 4;
 template <int W, int KPL>
 constexpr size_t pass1_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 2 + 1); }
@@ -668,8 +721,7 @@ constexpr size_t pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
 // stored contiguously at its own position, as if all runs were one.
 template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, TileStarts ts, u64 ntiles,
-                    TwoPass tp) {
+void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   static_assert(kTpCountTile % kTile == 0, "sub-tiles of a counting tile");
   extern __shared__ u64 lds64[];
@@ -685,17 +737,12 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nra
   const u32 fmask = tp.F - 1;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u32 q0 = wave * kSub + lane;
-  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
+  for (TileOrder o(tp.ntiles); o.t < o.end; o.t += o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kTpCountTile;
     const u32 ttn = (u32)min((u64)kTpCountTile, n - tbase);
-    // the tile's rows in fine bucket f follow those of the earlier tiles:
-    // fbase[f] + the earlier keys of the ranks r = c*F + f
-    if (threadIdx.x < tp.F) running[threadIdx.x] = (u32)tp.fbase[threadIdx.x];
-    __syncthreads();
-    const u64 crow = (t / kBucketChunk) * nranks, trow = t * nranks;
-    for (u32 r = threadIdx.x; r < nranks; r += kB)
-      atomicAdd(&running[r & fmask], ts.chunks[crow + r] + ts.counts[trow + r]);
+    // the tile's rows in fine bucket f follow those of the earlier tiles
+    if (threadIdx.x < tp.F) running[threadIdx.x] = (u32)tp.fbase[threadIdx.x] + tp.fine_before(t, threadIdx.x);
     for (u32 s0 = 0; s0 < ttn; s0 += kTile) {
       const u32 tn = min(kTile, ttn - s0);
       const u64 sbase = tbase + s0;
@@ -755,7 +802,7 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nra
 
 template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass2(FastMod rk, u32 nranks, TileStarts ts, TwoPass tp, Out out) {
+void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                    // [kTile] digests, then key pieces
@@ -775,18 +822,14 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TileStarts ts, TwoPass tp, Out out) 
     const u32 f = (u32)(o.t / tp.nsegf);
     const u64 g0 = (o.t % tp.nsegf) * tp.SG;
     const u64 g1 = min(g0 + tp.SG, tp.nchunks);
-    if (threadIdx.x < 2) seg[threadIdx.x] = 0;
-    __syncthreads();
+    if (threadIdx.x == 0) {
+      const u32 lo = tp.fine_before(g0 * kTpChunkTiles, f);
+      seg[0] = lo;
+      seg[1] = tp.fine_before(min(g1 * kTpChunkTiles, tp.ntiles), f) - lo;
+    }
     if (threadIdx.x < tp.C) {
       const u32 r = threadIdx.x * tp.F + f;
-      u32 lo = 0, cnt = 0;
-      if (r < nranks) {
-        lo = ts.chunks[g0 * nranks + r];
-        cnt = (u32)((g1 < tp.nchunks ? (u64)ts.chunks[g1 * nranks + r] : tp.totals[r]) - lo);
-        running[threadIdx.x] = (u32)ts.base[r] + lo;
-      }
-      atomicAdd(&seg[0], lo);
-      atomicAdd(&seg[1], cnt);
+      if (r < nranks) running[threadIdx.x] = (u32)tp.base[r] + tp.chunkcnt[g0 * nranks + r];
     }
     __syncthreads();
     const u32 sstart = (u32)tp.fbase[f] + seg[0], slen = seg[1];

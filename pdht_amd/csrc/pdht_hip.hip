@@ -963,8 +963,13 @@ namespace pdht {
 struct BucketWs {
   u32 *counts, *chunks;
   u64 *totals, *base, *fbase;
-  uint8_t *ikeys;  // two-pass intermediate (8/16/32-B keys): [n][keysize] key rows
-  u32 *iidx;       //   and [n] original indices
+  // two-pass sort (8/16/32-B keys): fine-bucket counts per tile and per
+  // 32-tile chunk, fine totals, rank counts per count-chunk, and the
+  // intermediate ([n][keysize] key rows + [n] original indices)
+  u32 *countsF, *chunksF, *chunkcnt;
+  u64 *totalsF;
+  uint8_t *ikeys;
+  u32 *iidx;
   size_t bytes;
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -988,6 +993,17 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
   w.fbase = reinterpret_cast<u64 *>(p + off);
   off += round256((size_t)kTpMaxDigits * 8);
   if (two_pass_keysize(keysize)) {
+    const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
+    const u64 tp_chunks32 = (tp_tiles + kBucketChunk - 1) / kBucketChunk;
+    const u64 tp_chunks = (tp_tiles + kTpChunkTiles - 1) / kTpChunkTiles;
+    w.countsF = reinterpret_cast<u32 *>(p + off);
+    off += round256((size_t)tp_tiles * kTpMaxDigits * 4);
+    w.chunksF = reinterpret_cast<u32 *>(p + off);
+    off += round256((size_t)tp_chunks32 * kTpMaxDigits * 4);
+    w.totalsF = reinterpret_cast<u64 *>(p + off);
+    off += round256((size_t)kTpMaxDigits * 8);
+    w.chunkcnt = reinterpret_cast<u32 *>(p + off);
+    off += round256((size_t)tp_chunks * nranks * 4);
     w.ikeys = p + off;
     off += round256(n * keysize);
     w.iidx = reinterpret_cast<u32 *>(p + off);
@@ -1092,10 +1108,10 @@ static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &ou
   const u64 cus = (u64)std::max(1, g_dev[dev].cus);
   unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU);
   if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
-  f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, a.nranks, a.ts, a.ntiles, tp);
+  f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp);
   unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
   if (g2 >= 8) g2 &= ~7u;
-  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, a.ts, tp, out);
+  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out);
   g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
   return 0;
 }
@@ -1181,7 +1197,44 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   a.ts = TileStarts{w.counts, w.chunks, w.base, nranks};
   a.ntiles = ntiles;
   const size_t hist_lds = (size_t)nranks * 4;
-  if (ntiles) {
+  TwoPass tp{};
+  if (kind == BucketKernel::kTwoPass) {
+    tp.fbits = (a.nbits + 1) / 2;
+    tp.F = 1u << tp.fbits;
+    tp.C = (nranks + tp.F - 1) >> tp.fbits;
+    tp.cbits = a.nbits - tp.fbits;
+    tp.countsF = w.countsF;
+    tp.chunksF = w.chunksF;
+    tp.totalsF = w.totalsF;
+    tp.chunkcnt = w.chunkcnt;
+    tp.base = w.base;
+    tp.fbase = w.fbase;
+    tp.ikeys = w.ikeys;
+    tp.iidx = w.iidx;
+    tp.ntiles = ntiles;
+    tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
+    tp.SG = std::max<u64>(1, tp.F / kTpChunkTiles);  // ~4096 keys per segment
+    tp.nsegf = (tp.nchunks + tp.SG - 1) / tp.SG;
+    tp.nseg = (u64)tp.F * tp.nsegf;
+  }
+  if (ntiles && kind == BucketKernel::kTwoPass) {
+    const u64 nchunks32 = (ntiles + kBucketChunk - 1) / kBucketChunk;
+    const unsigned gc = (unsigned)std::min<u64>(tp.nchunks, (u64)std::max(1, g_dev[dev].cus) * 8);
+    if (keysize == 8)
+      k_bucket_count_tp<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
+                                                          ntiles);
+    else if (keysize == 16)
+      k_bucket_count_tp<16><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
+                                                           ntiles);
+    else
+      k_bucket_count_tp<32><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
+                                                           ntiles);
+    k_bucket_colscan<<<dim3((tp.F + 63) / 64, (unsigned)nchunks32), 64, 0, st>>>(w.countsF, ntiles, tp.F,
+                                                                                   w.chunksF);
+    k_bucket_chunkscan<<<(tp.F + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunksF, nchunks32, tp.F, w.totalsF);
+    k_bucket_chunkscan<<<(nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunkcnt, tp.nchunks, nranks,
+                                                                        w.totals);
+  } else if (ntiles) {
     const unsigned gc = grid_for(ntiles, 8, dev);
     if (fixed && keysize == 8)
       k_bucket_count_reg<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
@@ -1199,23 +1252,8 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   } else {
     HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
   }
-  TwoPass tp{};
-  if (kind == BucketKernel::kTwoPass) {
-    tp.fbits = (a.nbits + 1) / 2;
-    tp.F = 1u << tp.fbits;
-    tp.C = (nranks + tp.F - 1) >> tp.fbits;
-    tp.cbits = a.nbits - tp.fbits;
-    tp.fbase = w.fbase;
-    tp.totals = w.totals;
-    tp.ikeys = w.ikeys;
-    tp.iidx = w.iidx;
-    tp.nchunks = nchunks;
-    tp.SG = std::max<u64>(1, tp.F / 32);  // ~4096 keys per segment
-    tp.nsegf = (nchunks + tp.SG - 1) / tp.SG;
-    tp.nseg = (u64)tp.F * tp.nsegf;
-  }
-  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, tp.fbits,
-                                      kind == BucketKernel::kTwoPass ? w.fbase : nullptr);
+  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, tp.fbits, w.totalsF,
+                                            kind == BucketKernel::kTwoPass ? w.fbase : nullptr);
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;

@@ -15,6 +15,7 @@ the two modulo reductions of hash.c:27 and :29 done in Python.
   python tests/golden/gen_golden.py --full   # + full-config fold checksums
   python tests/golden/gen_golden.py --extra  # + place/bucket/long folds (added)
   python tests/golden/gen_golden.py --r02    # + WeakHashLen32WithSeeds(6) vectors
+  python tests/golden/gen_golden.py --bucket8k  # + 8192-rank bucketing folds
                                              #   and cfg1 pdht_hash placement folds (added)
 """
 from __future__ import annotations
@@ -219,6 +220,28 @@ def folds_extra() -> dict:
     return res
 
 
+def folds_bucket8k() -> dict:
+    """bucket8k (8-B keys, nptes 3, nranks 8192: the two-pass bucketing path),
+    per 16M-key shard r = 0..7: folds of the stably bucketed mbits, of the
+    original indices and of the bucket offsets, from the reference CityHash64
+    plus hash.c:29's reduction."""
+    thr = os.cpu_count() or 8
+    res = {"n": 16 * M, "L": 8, "nptes": 3, "nranks": 8192, "shards": []}
+    n = 16 * M
+    for r in range(8):
+        keys = O.fixed_keys(n, 8, first_key=r * n)
+        m = O.apply_ref64(keys, n, L=8, threads=thr)
+        rk = (m % np.uint64(8192)).astype(np.int64)
+        order = np.argsort(rk, kind="stable")
+        offs = np.zeros(8193, np.uint64)
+        np.cumsum(np.bincount(rk, minlength=8192).astype(np.uint64), out=offs[1:])
+        res["shards"].append({"mbits": f"{O.fold64(m[order], 0):016x}",
+                              "index": f"{O.fold64(order.astype(np.uint64), 0):016x}",
+                              "offsets": f"{O.fold64(offs, 0):016x}"})
+        print(f"  bucket8k shard {r} done", flush=True)
+    return res
+
+
 def r02_vectors(R) -> dict:
     """WeakHashLen32WithSeeds6 / WeakHashLen32WithSeeds (city.c:173-198;
     exported by the reference although city.h does not declare them) on
@@ -265,11 +288,22 @@ def main():
                     help="add the place/bucket/long folds to config_folds.json")
     ap.add_argument("--r02", action="store_true",
                     help="add the WeakHash vectors (npz) and the cfg1 placement folds (json)")
+    ap.add_argument("--bucket8k", action="store_true",
+                    help="add the 8192-rank bucketing folds (json)")
     a = ap.parse_args()
     O.build()
     R = O.ref()
     if R is None:
         sys.exit("oracle/_ref not built: /root/reference is required to regenerate fixtures")
+    if a.bucket8k:
+        path = os.path.join(HERE, "config_folds.json")
+        with open(path) as f:
+            doc = json.load(f)
+        doc["configs"]["bucket_8B_16M_8192"] = folds_bucket8k()
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print("added bucket8k folds")
+        return
     if a.r02:
         npz = os.path.join(HERE, "city_golden.npz")
         with np.load(npz, allow_pickle=False) as z:

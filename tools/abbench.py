@@ -58,11 +58,11 @@ def workload(name, dev):
         outs = P.place_batch(keys, 1, 4, hist=hist)
         return ((lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)),
                 (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 80)
-    if name in ("cfg2", "cfg4", "long", "long64", "place", "bucket"):
-        L = {"cfg2": 64, "cfg4": 64, "long": 1024, "long64": 1024, "place": 8, "bucket": 8}[name]
-        n = M if name in ("long", "long64") else 16 * M
+    if name in ("cfg2", "cfg5", "cfg4", "long", "long64", "place", "bucket"):
+        L = {"cfg2": 64, "cfg5": 64, "cfg4": 64, "long": 1024, "long64": 1024, "place": 8, "bucket": 8}[name]
+        n = M if name in ("long", "long64") else 128 * M if name == "cfg5" else 16 * M
         keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
-        if name in ("cfg2", "long64"):
+        if name in ("cfg2", "cfg5", "long64"):
             out = torch.empty(n, dtype=torch.int64, device=dev)
             return (lambda: P.city64_batch(keys, out=out)), (lambda: out.clone()), n * (L + 8)
         if name in ("cfg4", "long"):
@@ -77,6 +77,8 @@ def workload(name, dev):
         outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
         return ((lambda: P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)),
                 (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (8 + 8 + 8 + 4 + 4))
+    if name not in ("cfg3", "cfg3c", "cfg3fold"):
+        raise SystemExit(f"unknown work {name}")
     n = 64 * M
     lo, hi = (136, 136) if name == "cfg3c" else (16, 256)
     lens = P.mixed_lengths(0x1E575EED1E575EED, 0, n, lo, hi, device=dev)
