@@ -234,14 +234,20 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
       // keys too long for a 64-key window: per-lane global reads (r01: an
       // LDS chunk-streaming kernel measured 0.36-0.47 of peak against this
       // kernel's 0.50-0.62 on 256 B - 8 KiB keys)
+      // 2 WG/CU: the per-lane walks of 64 keys touch 64 lines per wave
+      // instruction, and fewer waves keep more of those lines in L2 for the
+      // next 16-B pieces (r02, tools/abbench.py long64: 0.575 at 2 WG/CU
+      // against 0.535 at 8); the CRC path (LDS tables) is indifferent and
+      // keeps 8.
+      constexpr int kPerCu = kShort ? 2 : 8;
       if (al16 && stride % 16 == 0) {
-        g_kernel = "k_global<fixed,a16>@8";
-        k_global<false, Algo, SinkNt, true><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(
+        g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
+        k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, sink_nt);
       } else {
-        g_kernel = "k_global<fixed>@8";
-        k_global<false, Algo, SinkNt><<<grid_for(blocks, 8, dev), kBlock, 0, st>>>(k, nullptr, 0, stride,
-                                                                                    keylen, n, algo, sink_nt);
+        g_kernel = kShort ? "k_global<fixed>@2" : "k_global<fixed>@8";
+        k_global<false, Algo, SinkNt><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, sink_nt);
       }
     } else if (tile_bytes > kWinBytes) {
       g_kernel = "k_window<fixed,nt,16K>@2";

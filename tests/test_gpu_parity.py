@@ -59,13 +59,14 @@ SMALL_KERNELS = {8: "k_fixed_direct<8,4,nt-store>@8", 16: "k_fixed_direct<16,2,n
                  32: "k_fixed_direct<32,2>@8", 64: "k_fixed_xpose64<nt,d2>@3"}
 
 
-def fixed_kernel(L, stride=None, aligned=True):
+def fixed_kernel(L, stride=None, aligned=True, crc=False):
     """launch_fixed's choice for a generic length: the LDS window that holds a
     64-key tile (12 KiB or 16 KiB), else per-lane global reads (16-B loads
-    when every key starts 16-B aligned)."""
+    when every key starts 16-B aligned; 2 WG/CU, 8 with the LDS CRC tables)."""
     tile = 63 * (stride or L) + L + 16
     if tile > 16384:
-        return "k_global<fixed,a16>@8" if aligned and (stride or L) % 16 == 0 else "k_global<fixed>@8"
+        g = "k_global<fixed,a16>" if aligned and (stride or L) % 16 == 0 else "k_global<fixed>"
+        return g + ("@8" if crc and L > 900 else "@2")
     return "k_window<fixed,nt,16K>@2" if tile > 12288 else "k_window<fixed,nt,12K>@3"
 
 
@@ -125,7 +126,7 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
     kd = to_dev(k, dev)
     assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
-    assert P.last_kernel() == fixed_kernel(L)
+    assert P.last_kernel() == fixed_kernel(L, crc=True)
     s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
     got = u64(P.citycrc128_seed_batch(kd[:300], (s0, s1))).reshape(-1, 2)
     assert [tuple(int(x) for x in g) for g in got] == \
