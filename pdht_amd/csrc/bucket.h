@@ -232,8 +232,10 @@ __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restr
                                                               u64 *__restrict__ base,
                                                               u64 *__restrict__ offsets_out, u32 fbits,
                                                               const u64 *__restrict__ ftot,
-                                                              u64 *__restrict__ fbase) {
+                                                              u64 *__restrict__ fbase,
+                                                              u32 *__restrict__ tickets) {
   __shared__ u64 scratch[kBaseThreads / 64];
+  if (tickets && threadIdx.x < 16) tickets[threadIdx.x] = 0;  // per-XCD tile tickets of the scatter kernels
   constexpr u32 kMaxPer = kBucketMaxRanks / kBaseThreads;
   const u32 per = (nranks + kBaseThreads - 1) / kBaseThreads;
   const u32 lo = min(threadIdx.x * per, nranks), hi = min(lo + per, nranks);
@@ -525,11 +527,38 @@ constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL, bo
 // branch-free stores (r01), although the branch-free form has no SGPR spills:
 // the compiler then batches each array's stores, and the store order changes
 // how the runs meet in L2.
-template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false>
+// Work items [0, nitems) dealt to the 8 XCDs in contiguous ranges (workgroup
+// b on XCD b % 8) and handed out inside each range in order, one ticket
+// (vector atomic) per item: the items in flight on an XCD stay one
+// contiguous window however its workgroups drift.  Needs gridDim.x % 8 == 0
+// and zeroed tickets[8].
+struct XcdTickets {
+  u32 *tickets;
+  u64 lo, hi;
+  u32 x;
+  __device__ __forceinline__ XcdTickets(u32 *tk, u64 nitems) : tickets(tk) {
+    x = blockIdx.x % 8;
+    lo = x * nitems / 8;
+    hi = (x + 1) * nitems / 8;
+  }
+  // block-uniform; every thread must call it
+  __device__ __forceinline__ u64 next(u32 *slot) const {
+    if (threadIdx.x == 0) *slot = atomicAdd(&tickets[x], 1u);
+    __syncthreads();
+    return lo + *slot;
+  }
+};
+
+// DYN: tiles handed out by a per-XCD ticket (one vector atomic per tile)
+// instead of the static stride of TileOrder, so the tiles in flight on an XCD
+// stay one contiguous window however the workgroups drift: the runs of one
+// bucket from neighbouring tiles are written close in time and leave L2 as
+// whole lines.
+template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false, bool DYN = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(PACK ? 3 : (L == 8 || W == 8) ? 2 : 1)))
 void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, u32 nbits, TileStarts ts, u64 ntiles,
-    Out out) {
+    Out out, u32 *__restrict__ tickets = nullptr) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                              // [kTile]
@@ -544,7 +573,11 @@ void k_bucket_scatter_staged(
   u32 per = (nranks + kB - 1) / kB;
   if (PACK) per = (per + 1) & ~1u;
   const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
-  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
+  __shared__ u32 s_ticket;
+  const XcdTickets tk(tickets, ntiles);
+  TileOrder o(ntiles);
+  if constexpr (DYN) o.t = tk.next(&s_ticket), o.end = tk.hi;
+  for (; o.t < o.end; o.t = DYN ? tk.next(&s_ticket) : o.t + o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kTile;
     const u32 tn = (u32)min((u64)kTile, n - tbase);
@@ -719,9 +752,9 @@ constexpr size_t pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
 
 // DBG (tuning build only, timing-only, wrong results): 1 = every sub-tile
 // stored contiguously at its own position, as if all runs were one.
-template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0>
+template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0, bool DYN = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp) {
+void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp, u32 *__restrict__ tickets) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   static_assert(kTpCountTile % kTile == 0, "sub-tiles of a counting tile");
   extern __shared__ u64 lds64[];
@@ -737,7 +770,11 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass
   const u32 fmask = tp.F - 1;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u32 q0 = wave * kSub + lane;
-  for (TileOrder o(tp.ntiles); o.t < o.end; o.t += o.step) {
+  __shared__ u32 s_ticket;
+  const XcdTickets tk(tickets, tp.ntiles);
+  TileOrder o(tp.ntiles);
+  if constexpr (DYN) o.t = tk.next(&s_ticket), o.end = tk.hi;
+  for (; o.t < o.end; o.t = DYN ? tk.next(&s_ticket) : o.t + o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kTpCountTile;
     const u32 ttn = (u32)min((u64)kTpCountTile, n - tbase);
@@ -800,9 +837,9 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass
   }
 }
 
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0>
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0, bool DYN = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
+void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict__ tickets) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                    // [kTile] digests, then key pieces
@@ -818,7 +855,11 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
   const u32 q0 = wave * kSub + lane;
   const u32 fbits = tp.fbits;
   auto coarse = [&](u64 h) { return (u32)rk.mod(h) >> fbits; };
-  for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
+  __shared__ u32 s_ticket;
+  const XcdTickets tk(tickets, tp.nseg);
+  TileOrder o(tp.nseg);
+  if constexpr (DYN) o.t = tk.next(&s_ticket), o.end = tk.hi;
+  for (; o.t < o.end; o.t = DYN ? tk.next(&s_ticket) : o.t + o.step) {
     const u32 f = (u32)(o.t / tp.nsegf);
     const u64 g0 = (o.t % tp.nsegf) * tp.SG;
     const u64 g1 = min(g0 + tp.SG, tp.nchunks);

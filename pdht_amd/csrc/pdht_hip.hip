@@ -969,6 +969,7 @@ namespace pdht {
 struct BucketWs {
   u32 *counts, *chunks;
   u64 *totals, *base, *fbase;
+  u32 *tickets;  // [8] per-XCD tile tickets of the dynamic scatter
   // two-pass sort (8/16/32-B keys): fine-bucket counts per tile and per
   // 32-tile chunk, fine totals, rank counts per count-chunk, and the
   // intermediate ([n][keysize] key rows + [n] original indices)
@@ -998,6 +999,8 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
   off += round256((size_t)nranks * 8);
   w.fbase = reinterpret_cast<u64 *>(p + off);
   off += round256((size_t)kTpMaxDigits * 8);
+  w.tickets = reinterpret_cast<u32 *>(p + off);
+  off += 256;
   if (two_pass_keysize(keysize)) {
     const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
     const u64 tp_chunks32 = (tp_tiles + kBucketChunk - 1) / kBucketChunk;
@@ -1034,20 +1037,26 @@ struct BucketArgs {
   u64 ntiles;
 };
 
-template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL>
-static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
+template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL, bool DYN = false>
+static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev, u32 *tickets = nullptr) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
   static const char *const pnames[3] = {"k_bucket_scatter_staged<8B,u16>", "k_bucket_scatter_staged<16B,u16>",
                                         "k_bucket_scatter_staged<32B,u16>"};
   g_kernel = (PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
   const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK);
-  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK>;
+  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
   const int per_cu = bytes <= 53 * 1024 ? 3 : bytes <= 80 * 1024 ? 2 : 1;
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
   if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-  fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+  // (DYN: 8 XCD groups need a grid that is a multiple of 8; small grids use
+  // the static order)
+  if (DYN && g % 8 == 0)
+    fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, tickets);
+  else
+    k_bucket_scatter_staged<L, Out, W, KPL, PACK, false>
+        <<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, nullptr);
   return 0;
 }
 
@@ -1102,41 +1111,56 @@ static int launch_gather(const BucketArgs &a, const Out &out, u32 L, int lk, hip
 // faster for 8-B keys and at 8192 ranks 2.1x).
 static u32 two_pass_min_ranks(size_t keysize) { return keysize == 8 ? 1536 : keysize == 16 ? 1025 : 2049; }
 
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0>
-static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false>
+static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
+                           u32 *tickets) {
   static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
   constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;  // waves per SIMD
   const size_t b1 = pass1_lds_bytes<W, KPL>(), b2 = pass2_lds_bytes<W, KPL>();
-  auto f1 = &k_bucket_pass1<L, W, KPL, WPE, DBG>;
-  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG>;
+  auto f1 = &k_bucket_pass1<L, W, KPL, WPE, DBG, DYN>;
+  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, DYN>;
+  auto f1s = &k_bucket_pass1<L, W, KPL, WPE, DBG, false>;
+  auto f2s = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, false>;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f1s), b1)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f2s), b2)) return rc;
   const u64 cus = (u64)std::max(1, g_dev[dev].cus);
   unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU);
   if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
-  f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp);
+  // (tickets need a grid that is a multiple of 8; small grids: static order)
+  if (DYN && g1 % 8 == 0)
+    f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp, tickets);
+  else
+    f1s<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp, nullptr);
   unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
   if (g2 >= 8) g2 &= ~7u;
-  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out);
+  if (DYN && g2 % 8 == 0)
+    f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out, tickets + 8);
+  else
+    f2s<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out, nullptr);
   g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
   return 0;
 }
 
 template <int L, class Out>
-static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
+static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
+                               u32 *tickets) {
 #ifdef PDHT_HIP_TUNING
   // 73-76: sub-tile shape (waves x keys per lane) and workgroups per CU;
-  // 77: 73 with contiguous stores (timing-only, wrong results)
+  // 77: 73 with contiguous stores (timing-only, wrong results); 86: per-XCD
+  // tile tickets
   switch (tuning_variant()) {
-    case 73: return launch_two_pass<L, Out, 4, 8, 4>(a, tp, out, st, dev);
-    case 74: return launch_two_pass<L, Out, 8, 4, 4>(a, tp, out, st, dev);
-    case 75: return launch_two_pass<L, Out, 4, 16, 2>(a, tp, out, st, dev);
-    case 76: return launch_two_pass<L, Out, 4, 4, 6>(a, tp, out, st, dev);
-    case 77: return launch_two_pass<L, Out, 4, 8, 4, 1>(a, tp, out, st, dev);  // timing-only
+    case 73: return launch_two_pass<L, Out, 4, 8, 4>(a, tp, out, st, dev, tickets);
+    case 74: return launch_two_pass<L, Out, 8, 4, 4>(a, tp, out, st, dev, tickets);
+    case 75: return launch_two_pass<L, Out, 4, 16, 2>(a, tp, out, st, dev, tickets);
+    case 76: return launch_two_pass<L, Out, 4, 4, 6>(a, tp, out, st, dev, tickets);
+    case 77: return launch_two_pass<L, Out, 4, 8, 4, 1>(a, tp, out, st, dev, tickets);  // timing-only
+    case 86: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, true>(a, tp, out, st, dev, tickets);
     default: break;
   }
 #endif
-  return launch_two_pass<L, Out>(a, tp, out, st, dev);
+  return launch_two_pass<L, Out>(a, tp, out, st, dev, tickets);
 }
 
 enum class BucketKernel { kGather, kStaged, kReg, kGeneric, kTwoPass };
@@ -1259,7 +1283,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
   }
   k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, tp.fbits, w.totalsF,
-                                            kind == BucketKernel::kTwoPass ? w.fbase : nullptr);
+                                            kind == BucketKernel::kTwoPass ? w.fbase : nullptr, w.tickets);
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = 0;
@@ -1293,20 +1317,24 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
       unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * 2) & ~7u;
       fn<<<g, 512, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
-    } else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
+    } else if (kind == BucketKernel::kStaged && tuning_variant() == 85)  // static tile order (r02 default before)
+      rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
+                           : launch_staged<32, Out>(a, out, st, dev);
+    else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
       rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
                            : launch_staged<32, Out, true>(a, out, st, dev);
     else
 #endif
     if (kind == BucketKernel::kTwoPass)
-      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev)
-           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev)
-                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev);
-    else if (kind == BucketKernel::kStaged)
-      rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
-           : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
-                           : launch_staged<32, Out>(a, out, st, dev);
+      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev, w.tickets)
+                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev, w.tickets);
+    else if (kind == BucketKernel::kStaged)  // per-XCD tile tickets
+      rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets);
 #ifdef PDHT_HIP_TUNING
     else if (kind == BucketKernel::kReg)
       rc = keysize == 8 ? (waves == 8 ? launch_reg<8, 8, 16>(a, out, st, dev) : launch_reg<4, 8, 16>(a, out, st, dev))

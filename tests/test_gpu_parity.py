@@ -450,6 +450,10 @@ BUCKET_CASES += [(L, nr, n, v) for v in (54, 58) for L in (8, 13, 16) for nr in 
                  for n in (1, 16383, 16385, 1 << 20)]
 BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
+BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535)
+                 for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
+BUCKET_CASES += [(L, nr, n, 86) for L in (8, 16, 32) for nr in (2049, 8192)
+                 for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
 
 
 def _bucket_kernel(L, nranks, variant):
@@ -457,7 +461,8 @@ def _bucket_kernel(L, nranks, variant):
     register scatter above, the generic one for other lengths.  Tuning
     variants: 21 forces the generic-length kernel, 22 the register one, 54 the
     gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys),
-    70 one pass at any nranks, 71 two passes from 2 ranks up.  The product
+    70 one pass at any nranks, 71 two passes from 2 ranks up, 85 the staged
+    scatter in the static tile order instead of per-XCD tickets (same name).  The product
     sorts 8/16/32-B keys in two passes from 1536 / 1025 / 2049 ranks."""
     wg = "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
     if variant == 21:
@@ -543,6 +548,7 @@ RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 54, 58) for L in (8, 16, 32) fo
                  for n in (4097, 300007)]
 RECORD_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (7, 1000, 8192)
                  for n in (4097, 300007)]
+RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n in (4097, (2 << 20) + 9)]
 
 
 @pytest.mark.parametrize("L,nranks,n,variant", RECORD_CASES)
