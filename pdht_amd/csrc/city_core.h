@@ -424,6 +424,26 @@ constexpr Crc32c5Tables make_crc32c5_tables() {
 }
 __device__ __constant__ const Crc32c5Tables kCrc5Dev = make_crc32c5_tables();
 
+// 6-bit slices: 11 fields (10 x 6 bits + the top 4), 64-entry tables.  A
+// 64-word table spans each of the 64 LDS banks once, so random indices are
+// still conflict-free, and a word costs 11 lookups instead of 13.
+struct Crc32c6Tables {
+  u32 t[11][64];
+};
+constexpr Crc32c6Tables make_crc32c6_tables() {
+  Crc32c6Tables F{};
+  const Crc32cTables S = make_crc32c_tables();
+  for (u32 k = 0; k < 11; ++k)
+    for (u32 f = 0; f < 64; ++f) {
+      const u64 x = k < 10 || f < 16 ? (u64)f << (6 * k) : 0;
+      F.t[k][f] = S.t[7][x & 0xff] ^ S.t[6][(x >> 8) & 0xff] ^ S.t[5][(x >> 16) & 0xff] ^
+                  S.t[4][(x >> 24) & 0xff] ^ S.t[3][(x >> 32) & 0xff] ^ S.t[2][(x >> 40) & 0xff] ^
+                  S.t[1][(x >> 48) & 0xff] ^ S.t[0][x >> 56];
+    }
+  return F;
+}
+__device__ __constant__ const Crc32c6Tables kCrc6Dev = make_crc32c6_tables();
+
 // Where the tables live: CrcConstTab = the compile-time slicing-by-8 tables
 // (host; device constant memory); kernels.h adds the LDS copy of the 5-bit
 // tables for the GPU's long-key path.

@@ -72,7 +72,10 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // A16: every key starts 16-B aligned (fixed keys, aligned base and stride):
 // spans at 16-B aligned offsets load as dwordx4, a quarter of the
 // instructions (the CRC-256 rounds read 240-B blocks at multiples of 240).
-template <bool A16 = false>
+// NT (tuning): 1 = every dwordx4 span load non-temporal; 2 = all but the
+// span's last 128 B, so the line a long-key block shares with the next block
+// is the one kept in L2.
+template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
   const uint8_t *p;
   template <int N>
@@ -84,7 +87,7 @@ struct GlobalReaderT {
         Words<N / 4> w;
 #pragma unroll
         for (int j = 0; j < N / 16; ++j) {
-          const u32x4 v = q[j];
+          const u32x4 v = (NT == 1 || (NT == 2 && j < N / 16 - 8)) ? __builtin_nontemporal_load(q + j) : q[j];
           w.d[4 * j + 0] = v.x;
           w.d[4 * j + 1] = v.y;
           w.d[4 * j + 2] = v.z;
@@ -170,23 +173,48 @@ struct CrcLdsTab {
     return r;
   }
 };
-template <class Base>
-struct CrcLds : Base {
-  static constexpr bool kCrcLds = true;
-  const u32 *tab = nullptr;  // set by algo_init() inside the kernel
-  template <class R>
-  __device__ __forceinline__ typename Base::Out operator()(const R &r, u64 len) const;
+// The 6-bit-slice form (city_core.h Crc32c6Tables): 11 lookups per word.
+struct CrcLds6Tab {
+  const u32 *t;  // [11][64]
+  __device__ __forceinline__ u32 crc64(u64 x) const {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    u32 r = t[0 * 64 + (lo & 63)] ^ t[1 * 64 + ((lo >> 6) & 63)] ^ t[2 * 64 + ((lo >> 12) & 63)] ^
+            t[3 * 64 + ((lo >> 18) & 63)] ^ t[4 * 64 + ((lo >> 24) & 63)];
+    r ^= t[5 * 64 + (__builtin_amdgcn_alignbit(hi, lo, 30) & 63)];
+    r ^= t[6 * 64 + ((hi >> 4) & 63)] ^ t[7 * 64 + ((hi >> 10) & 63)] ^ t[8 * 64 + ((hi >> 16) & 63)] ^
+         t[9 * 64 + ((hi >> 22) & 63)] ^ t[10 * 64 + (hi >> 28)];
+    return r;
+  }
+};
+template <int SB>
+struct CrcLdsSlices;
+template <>
+struct CrcLdsSlices<5> {
+  typedef CrcLdsTab Tab;
+  static constexpr u32 kWords = 13 * 32;
+  __device__ static u32 word(u32 k) { return kCrc5Dev.t[k >> 5][k & 31]; }
 };
 template <>
-template <class R>
-__device__ __forceinline__ u128 CrcLds<AlgoCrc128>::operator()(const R &r, u64 len) const {
-  return crc128(r, len, CrcLdsTab{tab});
-}
-template <>
-template <class R>
-__device__ __forceinline__ u128 CrcLds<AlgoCrc128Seed>::operator()(const R &r, u64 len) const {
-  return crc128_seed(r, len, u128{this->lo, this->hi}, CrcLdsTab{tab});
-}
+struct CrcLdsSlices<6> {
+  typedef CrcLds6Tab Tab;
+  static constexpr u32 kWords = 11 * 64;
+  __device__ static u32 word(u32 k) { return kCrc6Dev.t[k >> 6][k & 63]; }
+};
+
+template <class Base, int SB = 6>
+struct CrcLds : Base {
+  static constexpr bool kCrcLds = true;
+  typedef CrcLdsSlices<SB> Slices;
+  const u32 *tab = nullptr;  // set by algo_init() inside the kernel
+  template <class R>
+  __device__ __forceinline__ typename Base::Out operator()(const R &r, u64 len) const {
+    typedef typename Slices::Tab Tab;
+    if constexpr (std::is_same<Base, AlgoCrc128>::value)
+      return crc128(r, len, Tab{tab});
+    else
+      return crc128_seed(r, len, u128{this->lo, this->hi}, Tab{tab});
+  }
+};
 
 template <class A, class = void>
 struct HasCrcLds {
@@ -201,8 +229,9 @@ struct HasCrcLds<A, decltype((void)A::kCrcLds)> {
 template <class Algo>
 __device__ __forceinline__ void algo_init(Algo &a) {
   if constexpr (HasCrcLds<Algo>::value) {
-    __shared__ u32 tab[13 * 32];
-    for (u32 k = threadIdx.x; k < 13 * 32; k += blockDim.x) tab[k] = kCrc5Dev.t[k >> 5][k & 31];
+    typedef typename Algo::Slices S;
+    __shared__ u32 tab[S::kWords];
+    for (u32 k = threadIdx.x; k < S::kWords; k += blockDim.x) tab[k] = S::word(k);
     __syncthreads();
     a.tab = tab;
   }
@@ -794,7 +823,7 @@ __global__ __launch_bounds__(kBlock) void k_window_db(const uint8_t *__restrict_
 // lane walks its own key straight from global memory (GlobalReader); the
 // other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
 // bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
-template <bool VAR, class Algo, class Sink, bool A16 = false>
+template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0>
 __global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -813,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ b
       st = i * stride;
       len = keylen;
     }
-    sink.put(i, algo(GlobalReaderT<A16>{bytes + st}, len));
+    sink.put(i, algo(GlobalReaderT<A16, NT>{bytes + st}, len));
   }
   sink.flush();
 }

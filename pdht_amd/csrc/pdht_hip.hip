@@ -241,6 +241,19 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
       // keeps 8.
       constexpr int kPerCu = kShort ? 2 : 8;
       if (al16 && stride % 16 == 0) {
+#ifdef PDHT_HIP_TUNING
+        if (tuning_variant() == 91 || tuning_variant() == 92) {  // nt span loads (all / all but the last line)
+          g_kernel = tuning_variant() == 91 ? "k_global<fixed,a16,nt>" : "k_global<fixed,a16,nt-head>";
+          if (tuning_variant() == 91)
+            k_global<false, Algo, SinkNt, true, 1><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          else
+            k_global<false, Algo, SinkNt, true, 2><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+#endif
         g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
         k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, sink_nt);
@@ -638,8 +651,13 @@ PDHT_API int pdht_city128_batch_var_dev(const void *bytes, size_t nbytes, const 
 PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
                                        uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
-  if (keylen > 900)  // CityHashCrc256 rounds: CRC-32C tables in LDS
+  if (keylen > 900) {  // CityHashCrc256 rounds: CRC-32C tables in LDS
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 90)  // 5-bit slices, 13 lookups per word (r02 before the 6-bit tables)
+      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 5>{}, Sink128{nullptr, out}, ST(s));
+#endif
     return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
+  }
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));
 }
 PDHT_API int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride, size_t keylen,
