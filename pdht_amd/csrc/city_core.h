@@ -264,6 +264,24 @@ PDHT_HD u64 city64_long_final(const LongState &st) {
   return mix16(mix16(st.v.lo, st.w.lo) + smix(st.y) * kK1 + st.z, mix16(st.v.hi, st.w.hi) + st.x);
 }
 
+// Readers that set kPairs read the >64-byte loop two rounds (128 B, a whole
+// line of a 128-B aligned key) per span.
+template <class R, class = void>
+struct ReaderPairs {
+  static constexpr bool value = false;
+};
+template <class R>
+struct ReaderPairs<R, decltype((void)R::kPairs)> {
+  static constexpr bool value = R::kPairs;
+};
+template <int W, int O, int N>
+PDHT_HD Words<N> sub_words(const Words<W> &q) {
+  Words<N> w;
+#pragma unroll
+  for (int j = 0; j < N; ++j) w.d[j] = q.d[O + j];
+  return w;
+}
+
 // city.c:224-263
 template <class R>
 PDHT_HD u64 city64(const R &s, u64 len) {
@@ -274,7 +292,15 @@ PDHT_HD u64 city64(const R &s, u64 len) {
   city64_long_init(s.template span<64>(n - 64), len, st);
   st.x += fetch64(s, 0);
   const u32 rounds = (u32)((len - 1) >> 6);
-  for (u32 r = 0; r < rounds; ++r) round64(st, s.template span<64>(r << 6));
+  u32 r = 0;
+  if constexpr (ReaderPairs<R>::value) {
+    for (; r + 1 < rounds; r += 2) {
+      const Words<32> q = s.template span<128>(r << 6);
+      round64(st, sub_words<32, 0, 16>(q));
+      round64(st, sub_words<32, 16, 16>(q));
+    }
+  }
+  for (; r < rounds; ++r) round64(st, s.template span<64>(r << 6));
   return city64_long_final(st);
 }
 
@@ -467,9 +493,58 @@ PDHT_HD u64 crc32c_u64(u64 crc, u64 v, const Tab &T = Tab{}) {
 // its six 40-byte CHUNKs work on compile-time offsets into it: one memory
 // round trip per block instead of one per chunk (the long-key kernels read
 // each lane's key straight from global memory, and waited on every chunk).
+// Readers that set kLines read the 240-B blocks of CityHashCrc256Long as
+// whole 128-B lines of the key: block k's load runs on to the end of the line
+// its last byte lies in, and that line's remainder (0..112 B, 16 B more per
+// block, period 8 blocks) is carried in registers into block k+1, so no line
+// is fetched twice (the plain form reads lines 1, 3, 5, 7 of a 1 KiB key in
+// two blocks: 1.5x the bytes).
+template <class R, class = void>
+struct ReaderLines {
+  static constexpr bool value = false;
+};
+template <class R>
+struct ReaderLines<R, decltype((void)R::kLines)> {
+  static constexpr bool value = R::kLines;
+};
+// Block at key offset o (o = 240k, C = 16 * (k mod 8) bytes of it carried):
+// loads [o + C, o + C + LB), LB = 256 (128 when C = 112).
+template <int C, class R>
+PDHT_HD void crc_block_lines(const R &s, u32 o, Words<28> &carry, Words<60> &q) {
+  constexpr int CD = C / 4, LB = C == 112 ? 128 : 256, USE = (240 - C) / 4, NC = (LB - (240 - C)) / 4;
+  const Words<LB / 4> ld = s.template span<LB>(o + C);
+#pragma unroll
+  for (int i = 0; i < 60; ++i) q.d[i] = i < CD ? carry.d[i < CD ? i : 0] : ld.d[i < CD ? 0 : i - CD];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) carry.d[i] = ld.d[USE + i];
+}
+template <class R>
+PDHT_HD void crc_block_lines_ph(const R &s, u32 o, u32 ph, Words<28> &carry, Words<60> &q) {
+  switch (ph) {
+    case 0: crc_block_lines<0>(s, o, carry, q); break;
+    case 1: crc_block_lines<16>(s, o, carry, q); break;
+    case 2: crc_block_lines<32>(s, o, carry, q); break;
+    case 3: crc_block_lines<48>(s, o, carry, q); break;
+    case 4: crc_block_lines<64>(s, o, carry, q); break;
+    case 5: crc_block_lines<80>(s, o, carry, q); break;
+    case 6: crc_block_lines<96>(s, o, carry, q); break;
+    default: crc_block_lines<112>(s, o, carry, q); break;
+  }
+}
+
 template <class R, class Tab = CrcConstTab>
 PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T = Tab{}) {
-  Words<60> q = s.template span<240>(0);  // block 0 (len >= 240)
+  // line form: block k ends at or before its line-aligned load end B(k) =
+  // 240k + 16(k mod 8) + 256 (or + 128); while B <= len the blocks stream as
+  // whole lines, after that (only near the key's end) as plain 240-B spans
+  Words<60> q;
+  Words<28> carry;
+  constexpr bool kLn = ReaderLines<R>::value;
+  auto line_end = [](u64 k) { return 240 * k + 16 * (k & 7) + ((k & 7) == 7 ? 128 : 256); };
+  if (kLn && line_end(0) <= len)
+    crc_block_lines<0>(s, 0, carry, q);
+  else
+    q = s.template span<240>(0);  // block 0 (len >= 240)
   u64 a = q.w64(56) + kK0;
   u64 b = q.w64(96) + kK0;
   u64 c = out[0] = mix16(b, len);
@@ -505,7 +580,12 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
   u64 rest = len - blocks * 240;
   for (u64 k = 0; k < blocks; ++k) {
     // (prefetching the next block as well measured equal, r02: 165 VGPRs)
-    if (k) q = s.template span<240>(o);
+    if (k) {
+      if (kLn && line_end(k) <= len)  // uniform for fixed-length batches
+        crc_block_lines_ph(s, o, (u32)k & 7, carry, q);
+      else
+        q = s.template span<240>(o);
+    }
     chunk_at(q, 0, 1, 1);
     chunk_at(q, 40, kK0, 0);
     chunk_at(q, 80, 1, 1);

@@ -72,15 +72,41 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // A16: every key starts 16-B aligned (fixed keys, aligned base and stride):
 // spans at 16-B aligned offsets load as dwordx4, a quarter of the
 // instructions (the CRC-256 rounds read 240-B blocks at multiples of 240).
-// NT (tuning): 1 = every dwordx4 span load non-temporal; 2 = all but the
-// span's last 128 B, so the line a long-key block shares with the next block
-// is the one kept in L2.
+// NT = kLongLines (the long-key kernels): every span a lane reads covers
+// whole 128-B lines of its key where the algorithm allows -- CityHash64's
+// long loop two rounds (128 B) per span (kPairs), CityHashCrc256's 240-B
+// blocks with the line remainder carried in registers (kLines) -- and 8-B
+// aligned spans load as dwordx2.  A lane's 8 dwordx4 pieces of one line then
+// leave together and meet in L2; split over two spans a compute round apart,
+// the line was fetched twice (tools/abbench.py long64: 0.577 -> 0.679, long:
+// 0.530 -> 0.567).
+// Tuning only: 1 = every dwordx4 span load non-temporal (2x slower: each
+// 16-B piece refetches its line); 2 = all but the span's last 128 B; 3 =
+// kLines alone; 4 = kPairs alone.
+constexpr int kLongLines = 5;
 template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
+  static constexpr bool kLines = NT == 3 || NT == kLongLines;
+  static constexpr bool kPairs = NT == 4 || NT == kLongLines;
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
+    if constexpr (A16 && (NT == 3 || NT == kLongLines) && N % 8 == 0 && N % 16 != 0) {
+      if ((a & 7) == 0) {
+        typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+        typedef const __attribute__((address_space(1))) u32x2 gu32x2;
+        gu32x2 *q = reinterpret_cast<gu32x2 *>(a);
+        Words<N / 4> w;
+#pragma unroll
+        for (int j = 0; j < N / 8; ++j) {
+          const u32x2 v = q[j];
+          w.d[2 * j] = v.x;
+          w.d[2 * j + 1] = v.y;
+        }
+        return w;
+      }
+    }
     if constexpr (A16 && N % 16 == 0) {
       if ((a & 15) == 0) {
         gu32x4 *q = reinterpret_cast<gu32x4 *>(a);

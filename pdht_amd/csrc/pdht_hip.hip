@@ -242,6 +242,27 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
       constexpr int kPerCu = kShort ? 2 : 8;
       if (al16 && stride % 16 == 0) {
 #ifdef PDHT_HIP_TUNING
+        if (tuning_variant() == 93) {  // CRC-256 blocks as whole lines
+          g_kernel = "k_global<fixed,a16,lines>";
+          k_global<false, Algo, SinkNt, true, 3><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+        if (tuning_variant() == 95) {  // CityHash64's long loop in 128-B spans
+          g_kernel = "k_global<fixed,a16,pairs>";
+          k_global<false, Algo, SinkNt, true, 4><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+        if (tuning_variant() == 96) {  // r02 before the line spans: 240-B / 64-B spans as the algorithm reads them
+          g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
+          k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
         if (tuning_variant() == 91 || tuning_variant() == 92) {  // nt span loads (all / all but the last line)
           g_kernel = tuning_variant() == 91 ? "k_global<fixed,a16,nt>" : "k_global<fixed,a16,nt-head>";
           if (tuning_variant() == 91)
@@ -254,8 +275,8 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
           return 0;
         }
 #endif
-        g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
-        k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+        g_kernel = kShort ? "k_global<fixed,a16,lines>@2" : "k_global<fixed,a16,lines>@8";
+        k_global<false, Algo, SinkNt, true, kLongLines><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, sink_nt);
       } else {
         g_kernel = kShort ? "k_global<fixed>@2" : "k_global<fixed>@8";

@@ -65,7 +65,7 @@ def fixed_kernel(L, stride=None, aligned=True, crc=False):
     when every key starts 16-B aligned; 2 WG/CU, 8 with the LDS CRC tables)."""
     tile = 63 * (stride or L) + L + 16
     if tile > 16384:
-        g = "k_global<fixed,a16>" if aligned and (stride or L) % 16 == 0 else "k_global<fixed>"
+        g = "k_global<fixed,a16,lines>" if aligned and (stride or L) % 16 == 0 else "k_global<fixed>"
         return g + ("@8" if crc and L > 900 else "@2")
     return "k_window<fixed,nt,16K>@2" if tile > 12288 else "k_window<fixed,nt,12K>@3"
 
@@ -117,7 +117,7 @@ def test_long_keys(dev, oracle, L, n):
     assert (u64(mb) == m2).all() and (rk.cpu().numpy().view(np.uint32) == r2).all()
 
 
-@pytest.mark.parametrize("L", [901, 1000, 4096])
+@pytest.mark.parametrize("L", [901, 1000, 1024, 1920, 2200, 4096])
 def test_crc128_long_keys_many_tiles(dev, oracle, L):
     """CityHashCrc256 rounds with the LDS CRC tables, every workgroup of the
     grid busy (k_global, 8 WG/CU) and a ragged tail; seeded variant too."""
