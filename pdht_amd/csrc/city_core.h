@@ -341,29 +341,18 @@ PDHT_HD u128 murmur128(const R &s, u64 len, u128 seed) {
   return u128{a ^ b, mix16(b, a)};
 }
 
-// city.c:310-376
+template <class R, class = void>
+struct ReaderOneCarry {
+  static constexpr bool value = false;
+};
 template <class R>
-PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
-  if (len < 128) return murmur128(s, len, seed);
-  LongState st;
-  st.x = seed.lo;
-  st.y = seed.hi;
-  st.z = len * kK1;
-  {
-    const Words<4> h = s.template span<16>(0);
-    st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + h.w64(0);
-    st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + h.w64(8);
-  }
-  st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
-  st.w.hi = rotr_nz(st.x + fetch64(s, 88), 53) * kK1;
-  u32 o = 0;
-  u64 rem = len;
-  do {
-    round64(st, s.template span<64>(o));
-    round64(st, s.template span<64>(o + 64));
-    o += 128;
-    rem -= 128;
-  } while (rem >= 128);
+struct ReaderOneCarry<R, decltype((void)R::kOneCarry)> {
+  static constexpr bool value = R::kOneCarry;
+};
+
+// city.c:330-366 tail (after the 128-byte loop) and finalisation
+template <class R>
+PDHT_HD u128 city128_finish(const R &s, u32 o, u64 rem, const LongState &st) {
   u64 x = st.x, y = st.y, z = st.z;
   u128 v = st.v, w = st.w;
   x += rotr_nz(v.lo + z, 49) * kK0;
@@ -383,11 +372,103 @@ PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
   return u128{mix16(x + v.hi, w.hi) + y, mix16(x + w.hi, y + v.hi)};
 }
 
+// city.c:310-376 for len >= 128 on kPairs readers, the hashed bytes starting
+// SH (0 or 16: CityHash128's seed bytes) into a key whose 128-B lines the
+// reader fetches whole.  Each 128-byte iteration is one line load: with SH =
+// 16 the iteration's bytes are the rest of line j (112 B, carried in
+// registers from the previous load) and the head of line j+1; the last
+// iteration loads only the 16 B it needs when line j+1 would pass the key.
+template <int SH, class R>
+PDHT_HD u128 city128_seed_lines(const R &b, u64 len, u128 seed) {
+  static_assert(SH == 0 || SH == 16, "seed bytes: none or 16");
+  const u64 total = len + SH;
+  LongState st;
+  st.x = seed.lo;
+  st.y = seed.hi;
+  st.z = len * kK1;
+  Words<32> l0 = b.template span<128>(0);  // total >= 128 + SH
+  st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + l0.w64(SH);
+  st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + l0.w64(SH + 8);
+  st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
+  st.w.hi = rotr_nz(st.x + l0.w64(SH + 88), 53) * kK1;
+  u32 o = 0;
+  u64 rem = len;
+  if constexpr (SH == 0) {
+    do {
+      if (o) l0 = b.template span<128>(o);
+      round64(st, sub_words<32, 0, 16>(l0));
+      round64(st, sub_words<32, 16, 16>(l0));
+      o += 128;
+      rem -= 128;
+    } while (rem >= 128);
+  } else {
+    // two carry arrays used in turn (a single one cost 28 register moves
+    // per iteration on the loop's back edge)
+    Words<28> ca = sub_words<32, 4, 28>(l0), cb;
+    auto iter = [&](const Words<28> &cin, Words<28> &cout) -> bool {
+      Words<32> q;
+#pragma unroll
+      for (int i = 0; i < 28; ++i) q.d[i] = cin.d[i];
+      if ((u64)o + 256 <= total) {  // uniform for fixed-length batches
+        const Words<32> ld = b.template span<128>(o + 128);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q.d[28 + i] = ld.d[i];
+        cout = sub_words<32, 4, 28>(ld);
+      } else {  // last iteration (the next would need o + 144 + 128 <= total)
+        const Words<4> t = b.template span<16>(o + 128);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q.d[28 + i] = t.d[i];
+      }
+      round64(st, sub_words<32, 0, 16>(q));
+      round64(st, sub_words<32, 16, 16>(q));
+      o += 128;
+      rem -= 128;
+      return rem >= 128;
+    };
+    if constexpr (ReaderOneCarry<R>::value) {  // tuning A/B: one carry array
+      while (iter(ca, cb)) ca = cb;
+    } else {
+      while (iter(ca, cb) && iter(cb, ca)) {
+      }
+    }
+  }
+  return city128_finish(Shifted<R>{b, (u32)SH}, o, rem, st);
+}
+
+// city.c:310-376
+template <class R>
+PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
+  if (len < 128) return murmur128(s, len, seed);
+  if constexpr (ReaderPairs<R>::value) return city128_seed_lines<0>(s, len, seed);
+  LongState st;
+  st.x = seed.lo;
+  st.y = seed.hi;
+  st.z = len * kK1;
+  {
+    const Words<4> h = s.template span<16>(0);
+    st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + h.w64(0);
+    st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + h.w64(8);
+  }
+  st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
+  st.w.hi = rotr_nz(st.x + fetch64(s, 88), 53) * kK1;
+  u32 o = 0;
+  u64 rem = len;
+  do {
+    round64(st, s.template span<64>(o));
+    round64(st, s.template span<64>(o + 64));
+    o += 128;
+    rem -= 128;
+  } while (rem >= 128);
+  return city128_finish(s, o, rem, st);
+}
+
 // city.c:378-400
 template <class R>
 PDHT_HD u128 city128(const R &s, u64 len) {
   if (len >= 16) {
     const Words<4> h = s.template span<16>(0);
+    if constexpr (ReaderPairs<R>::value)
+      if (len >= 144) return city128_seed_lines<16>(s, len - 16, u128{h.w64(0) ^ kK3, h.w64(8)});
     return city128_seed(Shifted<R>{s, 16}, len - 16, u128{h.w64(0) ^ kK3, h.w64(8)});
   }
   if (len >= 8) {

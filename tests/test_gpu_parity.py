@@ -81,7 +81,7 @@ def test_city64_every_length(dev, oracle, L):
 
 
 @pytest.mark.parametrize("L", [0, 1, 3, 8, 13, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 144, 200, 256,
-                               899, 900, 901, 960, 2000, 4096])
+                               271, 272, 400, 527, 528, 899, 900, 901, 960, 1023, 2000, 4096])
 def test_city128_crc128_lengths(dev, oracle, L):
     rng = np.random.default_rng(1000 + L)
     n = 70
@@ -133,7 +133,7 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
         [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:300]]
 
 
-@pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 300, 1200])
+@pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 256, 300, 384, 400, 1200])
 def test_seeded_batches(dev, oracle, L):
     rng = np.random.default_rng(77 + L)
     k = rng.integers(0, 256, (65, L), dtype=np.uint8)

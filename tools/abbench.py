@@ -58,6 +58,14 @@ def workload(name, dev):
         outs = P.place_batch(keys, 1, 4, hist=hist)
         return ((lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)),
                 (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 80)
+    if name in ("long128", "long128s"):  # 2M x 512 B CityHash128 (city.c:378-400) / WithSeed (:310-376)
+        n, L = 2 * M, 512
+        keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        if name == "long128":
+            return (lambda: P.city128_batch(keys, out=out)), (lambda: out.clone()), n * (L + 16)
+        return ((lambda: P.city128_seed_batch(keys, (0x0123456789ABCDEF, 0xFEDCBA9876543210), out=out)),
+                (lambda: out.clone()), n * (L + 16))
     if name in ("cfg2", "cfg5", "cfg4", "long", "long64", "place", "bucket"):
         L = {"cfg2": 64, "cfg5": 64, "cfg4": 64, "long": 1024, "long64": 1024, "place": 8, "bucket": 8}[name]
         n = M if name in ("long", "long64") else 128 * M if name == "cfg5" else 16 * M
