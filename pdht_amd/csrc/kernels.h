@@ -82,14 +82,16 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // 0.530 -> 0.567).
 // Tuning only: 1 = every dwordx4 span load non-temporal (2x slower: each
 // 16-B piece refetches its line); 2 = all but the span's last 128 B; 3 =
-// kLines alone; 4 = kPairs alone; 6 = kPairs with CityHash128's carry in
-// one register array (moves on the loop's back edge).
+// kLines alone; 4 = kPairs alone; 7 = kLongLines + CityHash128's 16-B
+// shifted loop on line spans as well (carry in registers); 6 = 7 with the
+// carry in one register array (moves on the loop's back edge).
 constexpr int kLongLines = 5;
 template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
-  static constexpr bool kLines = NT == 3 || NT == kLongLines;
-  static constexpr bool kPairs = NT == 4 || NT == 6 || NT == kLongLines;
+  static constexpr bool kLines = NT == 3 || NT == 7 || NT == kLongLines;
+  static constexpr bool kPairs = NT == 4 || NT == 6 || NT == 7 || NT == kLongLines;
   static constexpr bool kOneCarry = NT == 6;
+  static constexpr bool kLines16 = NT == 6 || NT == 7;
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {

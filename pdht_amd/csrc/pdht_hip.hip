@@ -249,8 +249,15 @@ static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n
           HIP_TRY(hipGetLastError());
           return 0;
         }
+        if (tuning_variant() == 98) {  // + CityHash128's shifted loop on line spans
+          g_kernel = "k_global<fixed,a16,lines16>";
+          k_global<false, Algo, SinkNt, true, 7><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
         if (tuning_variant() == 95 || tuning_variant() == 97) {  // 128-B spans (97: one carry array)
-          g_kernel = tuning_variant() == 95 ? "k_global<fixed,a16,pairs>" : "k_global<fixed,a16,pairs,1carry>";
+          g_kernel = tuning_variant() == 95 ? "k_global<fixed,a16,pairs>" : "k_global<fixed,a16,lines16,1carry>";
           if (tuning_variant() == 97)
             k_global<false, Algo, SinkNt, true, 6><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
                 k, nullptr, 0, stride, keylen, n, algo, sink_nt);
