@@ -675,11 +675,6 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
   auto chunk_at = [&](const Words<60> &w, u32 base, u64 mult, u32 flip) {
     chunk(w.w64(base), w.w64(base + 8), w.w64(base + 16), w.w64(base + 24), w.w64(base + 32), mult, flip);
   };
-  auto chunk_span = [&](u64 mult, u32 flip) {
-    const Words<10> w = s.template span<40>(o);
-    chunk(w.w64(0), w.w64(8), w.w64(16), w.w64(24), w.w64(32), mult, flip);
-    o += 40;
-  };
   const u64 blocks = len / 240;
   u64 rest = len - blocks * 240;
   for (u64 k = 0; k < blocks; ++k) {
@@ -698,10 +693,18 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
     chunk_at(q, 200, kK0, 0);
     o += 240;
   }
-  for (; rest >= 40; rest -= 40) chunk_span(kK0, 0);
-  if (rest > 0) {
-    o = o + (u32)rest - 40;
-    chunk_span(kK0, 0);
+  // city.c:443-453: rest / 40 whole chunks, then one ending at len when
+  // rest % 40 != 0 (rest < 240: at most 6).  Every chunk's load is issued
+  // before the first is mixed (one round trip instead of up to six).
+  {
+    const u32 nt = (u32)(rest / 40) + (rest % 40 ? 1u : 0u);
+    Words<10> tw[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if ((u32)k < nt) tw[k] = s.template span<40>((u32)k < rest / 40 ? o + 40u * k : (u32)len - 40u);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if ((u32)k < nt) chunk(tw[k].w64(0), tw[k].w64(8), tw[k].w64(16), tw[k].w64(24), tw[k].w64(32), kK0, 0);
   }
   j += i << 32;
   a = mix16(a, j);
