@@ -320,6 +320,54 @@ __device__ __forceinline__ void rank_groups(const Tab &run, u32 wave, const u32 
   for (int g = 0; g < KPL; ++g) lp[g] = (u32)__shfl((int)base[g], (int)(al[g] >> 8)) + (al[g] & 0xffu);
 }
 
+// rank_groups without the per-bit ballots: each lane of a group writes its
+// lane id into an LDS owner table at its bucket, reads it back, and only the
+// lanes that lost (their bucket is shared in the group) are resolved, one
+// shared bucket per step (readlane + one ballot).  64 keys over 1024 buckets
+// share ~2 buckets per group, against nbits = 10 ballots per group.  OB
+// groups at a time, each with its own table (own: the wave's [OB][nranks]
+// bytes), so one LDS round trip serves OB groups.
+template <int KPL, int OB, class Tab>
+__device__ __forceinline__ void rank_groups_owner(const Tab &run, u32 wave, const u32 (&rr)[KPL], u32 q0, u32 tn,
+                                                  uint8_t *own, u32 nranks, u32 (&lp)[KPL]) {
+  static_assert(KPL % OB == 0, "owner batches");
+  const u32 lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1;
+  u32 al[KPL], base[KPL];  // al = ahead | leader lane << 8
+#pragma unroll
+  for (int g0 = 0; g0 < KPL; g0 += OB) {
+#pragma unroll
+    for (int b = 0; b < OB; ++b)
+      if (q0 + (g0 + b) * 64 < tn) own[b * nranks + rr[g0 + b]] = (uint8_t)lane;
+    wave_lds_sync();
+    u32 ow[OB];
+#pragma unroll
+    for (int b = 0; b < OB; ++b) ow[b] = q0 + (g0 + b) * 64 < tn ? own[b * nranks + rr[g0 + b]] : lane;
+#pragma unroll
+    for (int b = 0; b < OB; ++b) {
+      const int g = g0 + b;
+      const bool valid = q0 + g * 64 < tn;
+      u64 same = valid ? 1ull << lane : 0ull;
+      u64 losers = __ballot(valid && ow[b] != lane);
+      while (losers) {  // wave-uniform
+        const u32 src = (u32)__builtin_ctzll(losers);
+        const u32 bk = (u32)__builtin_amdgcn_readlane((int)rr[g], (int)src);
+        const bool eq = valid && rr[g] == bk;
+        const u64 m = __ballot(eq);
+        if (eq) same = m;
+        losers &= ~m;
+      }
+      const u32 ahead = (u32)__builtin_popcountll(same & below);
+      al[g] = ahead | ((same ? (u32)__builtin_ctzll(same) : 0u) << 8);
+      base[g] = 0;
+      if (valid && ahead == 0) base[g] = run.add(wave, rr[g], (u32)__builtin_popcountll(same));
+    }
+    wave_lds_sync();  // the next batch rewrites the tables
+  }
+#pragma unroll
+  for (int g = 0; g < KPL; ++g) lp[g] = (u32)__shfl((int)base[g], (int)(al[g] >> 8)) + (al[g] & 0xffu);
+}
+
 // rank_groups in batches of B groups, writing each key's index straight into
 // the sorted-order table: B x 2 registers per lane instead of KPL x 3.
 template <int KPL, int B, class Tab>
@@ -519,9 +567,9 @@ __device__ __forceinline__ void staged_store(u64 *stage, const u32 *delta, u32 t
 // 8-B keys, 1024 ranks.
 constexpr int kStW = 4, kStKPL = 16;
 constexpr u32 kStTile = kStW * kStKPL * 64;
-constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL, bool PACK = false) {
+constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL, bool PACK = false, int OB = 0) {
   return (size_t)W * KPL * 64 * 10 + (PACK ? (size_t)W * ((nranks + 1) & ~1u) * 2 : (size_t)W * nranks * 4) +
-         (size_t)nranks * 4;
+         (size_t)nranks * 4 + (size_t)W * OB * nranks;
 }
 // Per-entry branches around the stores measured 12 % faster than clamped
 // branch-free stores (r01), although the branch-free form has no SGPR spills:
@@ -554,7 +602,7 @@ struct XcdTickets {
 // stay one contiguous window however the workgroups drift: the runs of one
 // bucket from neighbouring tiles are written close in time and leave L2 as
 // whole lines.
-template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false, bool DYN = false>
+template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false, bool DYN = false, int OB = 0>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(PACK ? 3 : (L == 8 || W == 8) ? 2 : 1)))
 void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, u32 nbits, TileStarts ts, u64 ntiles,
@@ -614,7 +662,11 @@ void k_bucket_scatter_staged(
     }
     __syncthreads();
     u32 lp[KPL];
-    rank_groups<KPL>(run, wave, rr, q0, tn, nbits, lp);
+    if constexpr (OB > 0)
+      rank_groups_owner<KPL, OB>(run, wave, rr, q0, tn,
+                                 reinterpret_cast<uint8_t *>(delta + nranks) + wave * OB * nranks, nranks, lp);
+    else
+      rank_groups<KPL>(run, wave, rr, q0, tn, nbits, lp);
 #pragma unroll
     for (int g = 0; g < KPL; ++g)
       if (q0 + g * 64 < tn) {

@@ -1087,15 +1087,17 @@ struct BucketArgs {
   u64 ntiles;
 };
 
-template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL, bool DYN = false>
+template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL, bool DYN = false, int OB = 0>
 static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev, u32 *tickets = nullptr) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
   static const char *const pnames[3] = {"k_bucket_scatter_staged<8B,u16>", "k_bucket_scatter_staged<16B,u16>",
                                         "k_bucket_scatter_staged<32B,u16>"};
-  g_kernel = (PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
-  const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK);
-  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN>;
+  static const char *const onames[3] = {"k_bucket_scatter_staged<8B,own>", "k_bucket_scatter_staged<16B,own>",
+                                        "k_bucket_scatter_staged<32B,own>"};
+  g_kernel = (OB ? onames : PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK, OB);
+  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN, OB>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
   const int per_cu = bytes <= 53 * 1024 ? 3 : bytes <= 80 * 1024 ? 2 : 1;
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
@@ -1105,7 +1107,7 @@ static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, in
   if (DYN && g % 8 == 0)
     fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, tickets);
   else
-    k_bucket_scatter_staged<L, Out, W, KPL, PACK, false>
+    k_bucket_scatter_staged<L, Out, W, KPL, PACK, false, OB>
         <<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, nullptr);
   return 0;
 }
@@ -1371,6 +1373,19 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
                            : launch_staged<32, Out>(a, out, st, dev);
+    else if (kind == BucketKernel::kStaged && (tuning_variant() == 87 || tuning_variant() == 88))
+      // owner-table ranking (rank_groups_owner), 4 / 2 groups per LDS round trip
+      rc = tuning_variant() == 87
+               ? (keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 4>(a, out, st, dev, w.tickets)
+                  : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 4>(a, out, st, dev, w.tickets)
+                                  : launch_staged<32, Out, false, kStW, kStKPL, true, 4>(a, out, st, dev, w.tickets))
+               : (keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
+                  : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
+                                  : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets));
+    else if (kind == BucketKernel::kStaged && tuning_variant() == 89)  // ballot ranking at any nranks (r02 before)
+      rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets);
     else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
       rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
@@ -1381,6 +1396,16 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev, w.tickets)
            : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev, w.tickets)
                            : launch_two_pass_sel<32, Out>(a, tp, out, st, dev, w.tickets);
+    else if (kind == BucketKernel::kStaged && std::is_same<Out, OutSoA>::value && nranks >= 512 &&
+             staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024)
+      // owner-table ranking (rank_groups_owner): from 512 buckets a 64-key
+      // group shares few enough buckets that resolving only those beats
+      // nbits ballots (tools/abbench.py: 8-B keys at 1024 ranks 0.302 ->
+      // 0.276 ms, 16-B 0.514 -> 0.444; slower at 256 ranks and for records);
+      // while two workgroups still fit a CU
+      rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets);
     else if (kind == BucketKernel::kStaged)  // per-XCD tile tickets
       rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)

@@ -452,17 +452,21 @@ BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in 
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
+BUCKET_CASES += [(L, nr, n, v) for v in (87, 89) for L in (8, 16, 32) for nr in (1, 7, 511, 512, 1000, 1535)
+                 for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 86) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
 
 
-def _bucket_kernel(L, nranks, variant):
+def _bucket_kernel(L, nranks, variant, records=False):
     """Product: the staged scatter for 8/16/32-B keys up to 2048 ranks, the
     register scatter above, the generic one for other lengths.  Tuning
     variants: 21 forces the generic-length kernel, 22 the register one, 54 the
     gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys),
     70 one pass at any nranks, 71 two passes from 2 ranks up, 85 the staged
-    scatter in the static tile order instead of per-XCD tickets (same name).  The product
+    scatter in the static tile order instead of per-XCD tickets, 87 / 89 the
+    staged scatter with owner-table / ballot ranking at any nranks (same
+    names; the product ranks by owner tables from 512 ranks).  The product
     sorts 8/16/32-B keys in two passes from 1536 / 1025 / 2049 ranks."""
     wg = "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
     if variant == 21:
@@ -477,7 +481,13 @@ def _bucket_kernel(L, nranks, variant):
         two_pass_from = {8: 1536, 16: 1025, 32: 2049}[L]
         if (variant == 71 and nranks >= 2) or (variant != 70 and nranks >= two_pass_from):
             return f"k_bucket_pass2<{L}B>"
-        return f"k_bucket_scatter_{'staged' if nranks <= 2048 else 'reg'}<{L}B>"
+        if nranks > 2048:
+            return f"k_bucket_scatter_reg<{L}B>"
+        # owner-table ranking: array outputs from 512 ranks while the LDS
+        # (40960 + 28 B per rank) leaves two workgroups per CU
+        own = variant == 87 or (variant not in (85, 89) and not records and 512 <= nranks
+                                and 40960 + 28 * nranks <= 80 * 1024)
+        return f"k_bucket_scatter_staged<{L}B{',own' if own else ''}>"
     return wg
 
 
