@@ -191,11 +191,6 @@ __device__ __forceinline__ u64 same_bucket_lanes(bool valid, u32 r, u32 nbits) {
   return same;
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Exclusive scan of one value per thread over an NW-wave workgroup.
 template <int NW, class T = u32>

@@ -31,6 +31,14 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBlock = 256;  // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 
+// Orders one wave's LDS writes before its later LDS reads (and the reverse)
+// without a workgroup barrier: waves own their LDS regions.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // --------------------------------------------------------------- readers ---
 // Key bytes in LDS at an arbitrary byte offset.  A span of N bytes is one run
 // of N/4+1 dword reads from one base address (ds_read2_b32 with immediate
@@ -845,6 +853,109 @@ __global__ __launch_bounds__(kBlock) void k_window_db(const uint8_t *__restrict_
     put_pending();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sink.flush();
+}
+
+// ------------------------- window kernel, next window prefetched in VGPRs ---
+// Offset-indexed keys, as k_window<WIN, true>, but the window of tile
+// t+nwaves is loaded into registers (plain dwordx4 loads, NP x 16 B per lane)
+// while tile t hashes out of the one LDS window, and written to LDS at the
+// top of the next step: the window's memory latency hides under a tile of
+// hashing at the LDS footprint (and occupancy) of the single-window kernel,
+// which the double-LDS-window kernel (k_window_db) halved.  Loads past the
+// window's last 16-B piece re-read that piece (clamped address: no load under
+// a lane-divergent branch, none outside the 16-B blocks holding key bytes).
+template <int WIN, class Algo, class Sink, bool LNT = true>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void k_window_rp(const uint8_t *__restrict__ bytes, const u64 *__restrict__ offsets, u64 obase, u64 n, Algo algo,
+                 Sink sink) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B pieces");
+  constexpr int NP = (WIN + 1023) / 1024;
+  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  algo_init(algo);
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *const lds = win_all + wave * (WIN / 4);
+  u32x4 *const lds4 = reinterpret_cast<u32x4 *>(lds);
+  const u64 base = (u64)(uintptr_t)bytes;
+  struct Geo {
+    u64 wlo, start, end;  // wlo absolute; start/end relative to bytes
+    u32 wbytes;
+  };
+  auto load_offs = [&](u64 t, u64 &a, u64 &hi) {
+    const u64 k0 = t << 6;
+    const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
+    a = offsets[(k0 + lane < n) ? k0 + lane : n];
+    hi = offsets[kend];
+  };
+  auto geometry = [&](u64 a, u64 hi) {
+    Geo g;
+    const u64 nb = __shfl_down(a, 1);
+    g.start = a - obase;
+    g.end = (lane == 63 ? hi : nb) - obase;
+    const u64 first = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)a) |
+                       ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(a >> 32)) << 32)) - obase;
+    const u64 whi = hi - obase;
+    g.wlo = (base + first) & ~(u64)15;
+    const u64 span = whi > first ? base + whi - g.wlo : 0;
+    g.wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    return g;
+  };
+  u32x4 pre[NP];
+  auto issue = [&](const Geo &g) {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>((uintptr_t)g.wlo);
+    const u32 last = g.wbytes ? (g.wbytes - 1) >> 4 : 0;  // last 16-B piece
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+      if ((u32)j * 1024 < g.wbytes) {  // wave-uniform
+        const u32 p = min((u32)(64 * j) + lane, last);
+        pre[j] = ld<LNT>(src + p);
+      }
+  };
+  auto stage = [&](const Geo &g) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+      if ((u32)j * 1024 < g.wbytes && (u32)(64 * j) + lane < (g.wbytes + 15) >> 4) lds4[64 * j + lane] = pre[j];
+  };
+  u64 t = (u64)blockIdx.x * kWavesPerBlock + wave;
+  if (t < ntiles) {
+    const u64 lastt = ntiles - 1;
+    u64 a, hi, an, hin;
+    load_offs(t, a, hi);
+    Geo g = geometry(a, hi), gn;
+    issue(g);
+    load_offs(min(t + nwaves, lastt), an, hin);
+    for (;;) {
+      stage(g);
+      wave_lds_sync();
+      const u64 tn = t + nwaves;
+      const bool more = tn < ntiles;  // wave-uniform
+      if (more) {
+        gn = geometry(an, hin);
+        issue(gn);  // in flight while tile t hashes
+        load_offs(min(tn + nwaves, lastt), an, hin);
+      }
+      const u64 i = (t << 6) + lane;
+      if (i < n) {
+        const u64 len = g.end - g.start;
+        typename Algo::Out h;
+        if (base + g.end - g.wlo <= g.wbytes)
+          h = algo(LdsReader{lds, (u32)(base + g.start - g.wlo)}, len);
+        else
+          h = algo(GlobalReader{bytes + g.start}, len);
+        sink.put(i, h);
+      }
+      wave_lds_sync();  // the window is rewritten by the next stage()
+      if (!more) break;
+      t = tn;
+      g = gn;
+    }
+  }
   sink.flush();
 }
 

@@ -354,6 +354,17 @@ static int launch_var(const void *bytes, u64 nbytes, const u64 *offsets, u64 oba
     HIP_TRY(hipGetLastError());
     return 0;
   }
+  if (tuning_variant() == 48 || tuning_variant() == 49) {  // next window prefetched in VGPRs (48: nt loads)
+    g_kernel = tuning_variant() == 48 ? "k_window_rp<10224,nt>@4" : "k_window_rp<10224>@4";
+    if (tuning_variant() == 48)
+      k_window_rp<10224, Algo, SinkNt, true><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                    sink_nt);
+    else
+      k_window_rp<10224, Algo, SinkNt, false><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                     sink_nt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   if (tuning_variant() == 30 || tuning_variant() == 31) {  // offsets prefetched one tile ahead
     if (tuning_variant() == 31 || wide) {
       g_kernel = "k_window_var<16K>@2";

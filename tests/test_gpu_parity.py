@@ -260,7 +260,8 @@ def test_var_golden_mixed(dev, golden, oracle):
     assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
 
 
-VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2"}
+VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2",
+               48: "k_window_rp<10224,nt>@4", 49: "k_window_rp<10224>@4"}
 
 
 def auto_var_kernel(total_bytes, n):
@@ -693,7 +694,7 @@ def test_cfg4_crc128_16M_full_fold(dev, folds):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-@pytest.mark.parametrize("variant", [0, 13])
+@pytest.mark.parametrize("variant", [0, 13, 48])
 def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     """8.7 GB of keys: offsets far past 2^31 and 2^32 (64-bit window math)."""
     f = folds["cfg3_city64_64M_mixed"]
