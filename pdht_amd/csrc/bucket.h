@@ -505,7 +505,7 @@ __device__ __forceinline__ void staged_store(u64 *stage, const u32 *delta, u32 t
     for (int jj = 0; jj < kPer; ++jj) {
       const u32 j = min(jj * kB + threadIdx.x, tn - 1);
       hv[jj] = stage[j];
-      gp[jj] = delta[dig(hv[jj])] + j;
+      gp[jj] = delta[dig(hv[jj], j)] + j;
       if (jj * kB + threadIdx.x < tn) out.head(gp[jj], idx(j));
     }
     __syncthreads();
@@ -525,7 +525,7 @@ __device__ __forceinline__ void staged_store(u64 *stage, const u32 *delta, u32 t
     const u32 j = jj * kB + threadIdx.x;
     if (j < tn) {
       const u64 hv = stage[j];
-      gp[jj] = delta[dig(hv)] + j;
+      gp[jj] = delta[dig(hv, j)] + j;
       out.meta(gp[jj], hv, idx(j));
     }
   }
@@ -662,6 +662,8 @@ void k_bucket_scatter_staged(
                                  reinterpret_cast<uint8_t *>(delta + nranks) + wave * OB * nranks, nranks, lp);
     else
       rank_groups<KPL>(run, wave, rr, q0, tn, nbits, lp);
+    // (staging the bucket as well, u16 per slot, so that the store phase
+    // reads it instead of reducing the digest again, measured slower: r02)
 #pragma unroll
     for (int g = 0; g < KPL; ++g)
       if (q0 + g * 64 < tn) {
@@ -670,7 +672,7 @@ void k_bucket_scatter_staged(
       }
     __syncthreads();
     staged_store<L, KPL, kB>(
-        stage, delta, tn, kr, lp, q0, [&](u64 hv) { return (u32)rk.mod(hv); },
+        stage, delta, tn, kr, lp, q0, [&](u64 hv, u32) { return (u32)rk.mod(hv); },
         [&](u32 j) { return tbase + sidx[j]; }, out);
     __syncthreads();
   }
@@ -901,7 +903,7 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u32 q0 = wave * kSub + lane;
   const u32 fbits = tp.fbits;
-  auto coarse = [&](u64 h) { return (u32)rk.mod(h) >> fbits; };
+  auto coarse = [&](u64 h, u32) { return (u32)rk.mod(h) >> fbits; };
   __shared__ u32 s_ticket;
   const XcdTickets tk(tickets, tp.nseg);
   TileOrder o(tp.nseg);
@@ -938,7 +940,7 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict
 #pragma unroll
       for (int g = 0; g < KPL; ++g) {
         h[g] = city64(kr[g], (u64)L);
-        cc[g] = coarse(h[g]);
+        cc[g] = coarse(h[g], 0u);
       }
       __syncthreads();
 #pragma unroll
@@ -960,7 +962,7 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict
         __shared__ u32 dbase[1];
         if (threadIdx.x == 0) dbase[0] = (u32)p0;
         __syncthreads();
-        staged_store<L, KPL, kB>(stage, dbase, tn, kr, lp, q0, [](u64) { return 0u; },
+        staged_store<L, KPL, kB>(stage, dbase, tn, kr, lp, q0, [](u64, u32) { return 0u; },
                                  [&](u32 j) { return (u64)sidx[j]; }, out);
       } else {
         staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);

@@ -1413,7 +1413,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       // group shares few enough buckets that resolving only those beats
       // nbits ballots (tools/abbench.py: 8-B keys at 1024 ranks 0.302 ->
       // 0.276 ms, 16-B 0.514 -> 0.444; slower at 256 ranks and for records);
-      // while two workgroups still fit a CU
+      // while two workgroups still fit a CU (<= 1462 ranks)
       rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
                            : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets);

@@ -453,7 +453,7 @@ BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in 
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
-BUCKET_CASES += [(L, nr, n, v) for v in (87, 89) for L in (8, 16, 32) for nr in (1, 7, 511, 512, 1000, 1535)
+BUCKET_CASES += [(L, nr, n, v) for v in (87, 89) for L in (8, 16, 32) for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 86) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
