@@ -1106,7 +1106,10 @@ static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, in
                                         "k_bucket_scatter_staged<32B,u16>"};
   static const char *const onames[3] = {"k_bucket_scatter_staged<8B,own>", "k_bucket_scatter_staged<16B,own>",
                                         "k_bucket_scatter_staged<32B,own>"};
-  g_kernel = (OB ? onames : PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
+  static const char *const o8names[3] = {"k_bucket_scatter_staged<8B,own,8x16>",
+                                         "k_bucket_scatter_staged<16B,own,8x16>",
+                                         "k_bucket_scatter_staged<32B,own,8x16>"};
+  g_kernel = (OB ? (W == 8 ? o8names : onames) : PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
   const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK, OB);
   auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN, OB>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
@@ -1228,6 +1231,15 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
 
 enum class BucketKernel { kGather, kStaged, kReg, kGeneric, kTwoPass };
 
+enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16, kOwner4x24 };
+template <class Out>
+static StagedShape staged_shape(size_t keysize, u32 nranks) {
+  if (!std::is_same<Out, OutSoA>::value || nranks < 512) return StagedShape::kBallot4x16;
+  if (keysize != 32 && staged_lds_bytes(nranks, 8, 16, false, 2) <= 160 * 1024) return StagedShape::kOwner8x16;
+  if (staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024) return StagedShape::kOwner4x16;
+  return StagedShape::kBallot4x16;
+}
+
 // Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
 // (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
 // out_al: alignment bits of the output key rows (0 when they are 8-B aligned
@@ -1272,11 +1284,25 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   if (tuning_variant() == 52) ga_w = 4;
   if (tuning_variant() == 53) ga_kpl = 16;
 #endif
+  // Staged scatter shape (tools/abbench.py): owner-table
+  // ranking for array outputs from 512 ranks; with it, 8 waves x 16 keys per
+  // lane (8192-key tiles, 1 WG/CU) for 8/16-B keys while the LDS holds
+  // (8-B keys at 1024 ranks 0.274 -> 0.261 ms, 16-B 0.443 -> 0.405; 32-B
+  // keys lose 11 % and keep 4 x 16); else 4 x 16 while two workgroups fit a
+  // CU (<= 1462 ranks); ballots below 512 ranks and for records.
+  StagedShape shape = staged_shape<Out>(keysize, nranks);
+#ifdef PDHT_HIP_TUNING
+  if (tuning_variant() == 83) shape = StagedShape::kOwner8x16;
+  if (tuning_variant() == 87) shape = StagedShape::kOwner4x16;
+  if (tuning_variant() == 84 && keysize == 8) shape = StagedShape::kOwner4x24;
+  if (tuning_variant() == 85 || tuning_variant() == 89) shape = StagedShape::kBallot4x16;
+#endif
+  const u64 st_tile = shape == StagedShape::kOwner8x16 ? 8192 : shape == StagedShape::kOwner4x24 ? 6144 : kStTile;
   const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
   const int reg_kpl = keysize == 32 ? 8 : 16;
   const u64 tile = kind == BucketKernel::kGather     ? (u64)ga_w * ga_kpl * 64
                    : kind == BucketKernel::kTwoPass ? kTpCountTile
-                   : kind == BucketKernel::kStaged   ? kStTile
+                   : kind == BucketKernel::kStaged   ? st_tile
                    : kind == BucketKernel::kReg    ? (u64)waves * reg_kpl * 64
                                                    : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
@@ -1384,19 +1410,6 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
                            : launch_staged<32, Out>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged && (tuning_variant() == 87 || tuning_variant() == 88))
-      // owner-table ranking (rank_groups_owner), 4 / 2 groups per LDS round trip
-      rc = tuning_variant() == 87
-               ? (keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 4>(a, out, st, dev, w.tickets)
-                  : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 4>(a, out, st, dev, w.tickets)
-                                  : launch_staged<32, Out, false, kStW, kStKPL, true, 4>(a, out, st, dev, w.tickets))
-               : (keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
-                  : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
-                                  : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets));
-    else if (kind == BucketKernel::kStaged && tuning_variant() == 89)  // ballot ranking at any nranks (r02 before)
-      rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
-           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
-                           : launch_staged<32, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets);
     else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
       rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
@@ -1407,16 +1420,18 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev, w.tickets)
            : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev, w.tickets)
                            : launch_two_pass_sel<32, Out>(a, tp, out, st, dev, w.tickets);
-    else if (kind == BucketKernel::kStaged && std::is_same<Out, OutSoA>::value && nranks >= 512 &&
-             staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024)
-      // owner-table ranking (rank_groups_owner): from 512 buckets a 64-key
-      // group shares few enough buckets that resolving only those beats
-      // nbits ballots (tools/abbench.py: 8-B keys at 1024 ranks 0.302 ->
-      // 0.276 ms, 16-B 0.514 -> 0.444; slower at 256 ranks and for records);
-      // while two workgroups still fit a CU (<= 1462 ranks)
+    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner8x16)
+      rc = keysize == 8    ? launch_staged<8, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets);
+    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner4x16)
       rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
                            : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets);
+#ifdef PDHT_HIP_TUNING
+    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner4x24)  // slower (spills)
+      rc = launch_staged<8, Out, false, 4, 24, true, 2>(a, out, st, dev, w.tickets);
+#endif
     else if (kind == BucketKernel::kStaged)  // per-XCD tile tickets
       rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)

@@ -453,7 +453,8 @@ BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in 
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
-BUCKET_CASES += [(L, nr, n, v) for v in (87, 89) for L in (8, 16, 32) for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
+BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
+                 for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 86) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
@@ -465,9 +466,9 @@ def _bucket_kernel(L, nranks, variant, records=False):
     variants: 21 forces the generic-length kernel, 22 the register one, 54 the
     gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys),
     70 one pass at any nranks, 71 two passes from 2 ranks up, 85 the staged
-    scatter in the static tile order instead of per-XCD tickets, 87 / 89 the
-    staged scatter with owner-table / ballot ranking at any nranks (same
-    names; the product ranks by owner tables from 512 ranks).  The product
+    scatter in the static tile order instead of per-XCD tickets, 83 / 87 / 89
+    the staged scatter with owner-table ranking on 8 x 16 / 4 x 16 tiles or
+    with ballots, at any nranks.  The product
     sorts 8/16/32-B keys in two passes from 1536 / 1025 / 2049 ranks."""
     wg = "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
     if variant == 21:
@@ -484,11 +485,21 @@ def _bucket_kernel(L, nranks, variant, records=False):
             return f"k_bucket_pass2<{L}B>"
         if nranks > 2048:
             return f"k_bucket_scatter_reg<{L}B>"
-        # owner-table ranking: array outputs from 512 ranks while the LDS
-        # (40960 + 28 B per rank) leaves two workgroups per CU
-        own = variant == 87 or (variant not in (85, 89) and not records and 512 <= nranks
-                                and 40960 + 28 * nranks <= 80 * 1024)
-        return f"k_bucket_scatter_staged<{L}B{',own' if own else ''}>"
+        # staged_shape(): owner-table ranking for array outputs from 512
+        # ranks, on 8 x 16 tiles for 8/16-B keys while 81920 + 52 B per rank
+        # of LDS fits a CU, else on 4 x 16 tiles while 40960 + 28 B per rank
+        # leaves two workgroups per CU; ballots otherwise
+        if variant == 83:
+            return f"k_bucket_scatter_staged<{L}B,own,8x16>"
+        if variant == 87:
+            return f"k_bucket_scatter_staged<{L}B,own>"
+        if variant in (85, 89) or records or nranks < 512:
+            return f"k_bucket_scatter_staged<{L}B>"
+        if L != 32 and 81920 + 52 * nranks <= 160 * 1024:
+            return f"k_bucket_scatter_staged<{L}B,own,8x16>"
+        if 40960 + 28 * nranks <= 80 * 1024:
+            return f"k_bucket_scatter_staged<{L}B,own>"
+        return f"k_bucket_scatter_staged<{L}B>"
     return wg
 
 
