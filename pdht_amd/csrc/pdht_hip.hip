@@ -1234,7 +1234,15 @@ enum class BucketKernel { kGather, kStaged, kReg, kGeneric, kTwoPass };
 enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16, kOwner4x24 };
 template <class Out>
 static StagedShape staged_shape(size_t keysize, u32 nranks) {
-  if (!std::is_same<Out, OutSoA>::value || nranks < 512) return StagedShape::kBallot4x16;
+  if (nranks < 512) return StagedShape::kBallot4x16;
+  if (!std::is_same<Out, OutSoA>::value) {
+    // records: owner ranking pays for 16/32-B keys only (ab_records_*_shapes.log:
+    // 16-B at 1024 ranks 0.62 -> 0.56 ms, 32-B 1.29 -> 1.20); 8-B records
+    // lose 3 % with it
+    if (keysize != 8 && staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024)
+      return StagedShape::kOwner4x16;
+    return StagedShape::kBallot4x16;
+  }
   if (keysize != 32 && staged_lds_bytes(nranks, 8, 16, false, 2) <= 160 * 1024) return StagedShape::kOwner8x16;
   if (staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024) return StagedShape::kOwner4x16;
   return StagedShape::kBallot4x16;
