@@ -6,8 +6,10 @@
 
 One step = one pass of the hot path (one kernel launch) over this GPU's batch
 of synthetic keys already resident in HBM.  Default workload = BASELINE
-configs[1] ("cfg2": 16M x 64 B keys per GPU, CityHash64).  For N > 1 (launched
-by torch.distributed.run, one rank per GPU) rank r hashes its own contiguous
+configs[1] ("cfg2": 16M x 64 B keys per GPU, CityHash64).  For N > 1 (one rank
+per GPU: `python bench.py --gpus N` starts the N ranks itself through
+torch.distributed.run; under an external launcher WORLD_SIZE must equal N)
+rank r hashes its own contiguous
 slice [r*n, (r+1)*n) of the same key stream (pdht_amd.dist.weak_shard): no
 collective on the data path (weak scaling); the only collectives are the
 timing barrier, the max of elapsed times and the parity reductions.
@@ -61,7 +63,9 @@ METRIC = "Gkeys/s and achieved HBM GB/s, device-resident batch CityHash64 on 64B
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of this node; without WORLD_SIZE in the environment and N > 1 "
+                         "bench.py starts the N ranks itself (torch.distributed.run, 127.0.0.1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
@@ -72,7 +76,74 @@ def parse():
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.5,
                     help="wall budget of one CPU-baseline pass (best of 5 passes)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check only: every rank joins a gloo group, touches no GPU and rank 0 "
+                         "prints one JSON line with the world (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` started as one process: start the N ranks (one per
+    GPU) with torch.distributed.run and relay rank 0's JSON line.  This parent
+    never touches a GPU (no torch import at all): it only forwards the ranks'
+    other output to stderr and exits with the launcher's return code, which is
+    non-zero as soon as any rank failed.  The ranks rendezvous on 127.0.0.1."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{"):
+            try:
+                if isinstance(json.loads(s), dict):
+                    lines.append(s)
+                    continue
+            except ValueError:
+                pass
+        sys.stderr.write(line)
+    rc = p.wait()
+    for s in lines:
+        print(s, flush=True)
+    if rc == 0 and len(lines) != 1:
+        sys.stderr.write(f"bench.py: expected one JSON line from rank 0, got {len(lines)}\n")
+        return 1
+    return rc
+
+
+def dry_run(a) -> None:
+    """Launch check without a GPU: a gloo group of all ranks, every rank's
+    (rank, local rank, pid) gathered, one JSON line from rank 0."""
+    import torch.distributed as dist
+    from pdht_amd import dist as D
+    rank, local, world = D.env_rank_world()
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = {"rank": rank, "local_rank": local, "pid": os.getpid()}
+    allr = [mine]
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world, "ranks": allr,
+                          "gpus_arg": a.gpus, "backend": dist.get_backend() if world > 1 else None}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def golden_folds():
@@ -85,6 +156,17 @@ def golden_folds():
 
 def main():
     a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if a.gpus is not None and int(env_world) != a.gpus:
+            sys.stderr.write(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}: refusing to run a "
+                             f"different world than asked for\n")
+            sys.exit(2)
+    elif a.gpus is not None and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))  # before anything touches a GPU
+    if a.dry_run:
+        dry_run(a)
+        return
     import torch
     import torch.distributed as dist
 
@@ -224,7 +306,8 @@ def main():
         words = P.splitmix64_fill(SEED_KEYS, rank << 40, (total + 7) // 8 + 2, device=dev)
         data = words.view(torch.uint8)[:total]
         out = torch.empty(n, dtype=torch.int64, device=dev)
-        step = lambda: P.city64_var_batch(data, offs, out=out)  # noqa: E731
+        P.city64_var_batch(data, offs, out=out)  # offsets bounds-checked once ...
+        step = lambda: P.city64_var_batch(data, offs, out=out, check=False)  # noqa: E731  ... not per step
         bytes_per_key = total / n + 8 + 8
         total_bytes_in = total
         workload = f"cfg3: CityHash64 over {n >> 20}M mixed 16..256B keys per GPU (offset-indexed)"
@@ -285,7 +368,7 @@ def main():
                for _ in range(5)]
         for s, e in cev:
             s.record()
-            P.key_stream_var(data, offs, out=fold)
+            P.key_stream_var(data, offs, out=fold, check=False)
             e.record()
         torch.cuda.synchronize()
         cms = float(np.median([s.elapsed_time(e) for s, e in cev]))

@@ -36,6 +36,11 @@ extern "C" {
 
 #define PDHT_HIP_OK 0
 #define PDHT_HIP_ERROR 1 /* == PdhtStatusError */
+/* ABI revision of this header; pdht_hip_version() names the same number
+ * ("abi 3").  Revision 2 changed index_out to uint32_t, gave
+ * pdht_bucket_workspace_bytes its keysize and the *_var_dev entry points
+ * their nbytes: a caller built against an older header must be rebuilt. */
+#define PDHT_HIP_ABI_VERSION 3
 
 typedef struct ihipStream_t *pdht_hip_stream_t; /* layout of hipStream_t */
 
@@ -114,8 +119,9 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * nptes == 1 (pdht's default, pdht_impl.h:41) every ptindex is 0 and
  * ptindex_out is best NULL.  nranks <= 8192, n < 2^32.  `workspace`
  * (device) must hold pdht_bucket_workspace_bytes(n, keysize, nranks): the
- * per-tile counts and, for 8/16/32-B keys, the intermediate of the two-pass
- * sort used from 256 ranks up (n x (keysize + 4) bytes). */
+ * per-tile counts and, for 8/16/32-B keys at the rank counts that take the
+ * two-pass sort (from 1536 / 1025 / 2049 ranks for 8 / 16 / 32-B keys), its
+ * intermediate (n x (keysize + 4) bytes). */
 size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint32_t nptes, uint32_t nranks, void *workspace,

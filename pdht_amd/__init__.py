@@ -35,7 +35,7 @@ __all__ = [
     "citycrc128_batch_host", "place_batch_host", "splitmix64_fill", "mixed_lengths",
     "device_count", "PdhtTable", "K2", "bucket_batch", "bucket_records", "record_fields",
     "bucket_record_bytes", "bucket_workspace_bytes", "WeakHashLen32WithSeeds", "WeakHashLen32WithSeeds6",
-    "tuning", "last_kernel",
+    "tuning", "last_kernel", "mpi_lib",
 ]
 
 K2 = 0x9AE16A3B2F90404F  # city.c:96 (CityHash64WithSeed's seed0)
@@ -156,6 +156,19 @@ def lib():
         _product = _load(LIB_PATH)
         _lib = _product
     return _lib
+
+
+_mpi = None
+
+
+def mpi_lib():
+    """libpdht_hip_mpi.so: the same engine with the libmpipdht flavour of
+    pdht_hash / pdht_hash_batch(_dev) (libmpipdht/hash.c:6-9: mbits and rank,
+    ptindex never written).  Loaded on demand, beside the product library."""
+    global _mpi
+    if _mpi is None:
+        _mpi = _load(MPI_LIB_PATH)
+    return _mpi
 
 
 class tuning:
@@ -377,20 +390,33 @@ def city64_seed_batch(keys, seed: int, out=None, stream=None):
     return city64_seeds_batch(keys, K2, seed, out, stream)
 
 
-def _check_var(data, offsets):
+def _check_var(data, offsets, check=True):
     """(n, nbytes): nbytes = the data buffer's size, the bound of the key
-    bytes the batch spans (sizes the kernel's LDS window; never addresses)."""
+    bytes the batch spans (sizes the kernel's LDS window; never addresses).
+    check: also read offsets[0] and offsets[n] back (one 16-B D2H copy, which
+    synchronises with the stream) and require 0 <= offsets[0] <= offsets[n]
+    <= data.numel(), so that a bad offsets tensor raises instead of sending
+    the window kernel past the data buffer.  Skipped while the stream is being
+    captured into a graph, and with check=False (the caller vouches for the
+    offsets, e.g. a timed loop over offsets it has already checked); the
+    kernels trust that offsets never decrease, as the reference trusts its key
+    pointers."""
     torch = _torch()
     if data.dtype != torch.uint8 or not data.is_cuda or not data.is_contiguous():
         raise ValueError("data must be a contiguous CUDA uint8 tensor")
     _need(offsets, "offsets", torch.int64, data.device)
     if offsets.dim() != 1 or offsets.numel() < 1:
         raise ValueError("offsets must be a 1-D int64 tensor of n+1 entries")
-    return offsets.numel() - 1, data.numel()
+    n = offsets.numel() - 1
+    if check and n and not torch.cuda.is_current_stream_capturing():
+        lo, hi = (int(x) for x in offsets[[0, n]].tolist())
+        if not 0 <= lo <= hi <= data.numel():
+            raise ValueError(f"offsets span bytes [{lo}, {hi}) but data holds {data.numel()}")
+    return n, data.numel()
 
 
-def city64_var_batch(data, offsets, out=None, stream=None):
-    n, nb = _check_var(data, offsets)
+def city64_var_batch(data, offsets, out=None, stream=None, check=True):
+    n, nb = _check_var(data, offsets, check)
     out = _out(n, 1, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_city64_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
@@ -416,8 +442,8 @@ def city128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
     return out
 
 
-def city128_var_batch(data, offsets, out=None, stream=None):
-    n, nb = _check_var(data, offsets)
+def city128_var_batch(data, offsets, out=None, stream=None, check=True):
+    n, nb = _check_var(data, offsets, check)
     out = _out(n, 2, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_city128_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
@@ -443,8 +469,8 @@ def citycrc128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
     return out
 
 
-def citycrc128_var_batch(data, offsets, out=None, stream=None):
-    n, nb = _check_var(data, offsets)
+def citycrc128_var_batch(data, offsets, out=None, stream=None, check=True):
+    n, nb = _check_var(data, offsets, check)
     out = _out(n, 2, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_citycrc128_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out),
@@ -630,9 +656,9 @@ def key_stream(keys, out=None, stream=None):
     return out
 
 
-def key_stream_var(data, offsets, out=None, stream=None):
+def key_stream_var(data, offsets, out=None, stream=None, check=True):
     """Calibration: the variable-length kernel's data movement with an XOR fold."""
-    n, nb = _check_var(data, offsets)
+    n, nb = _check_var(data, offsets, check)
     out = _out(n, 1, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_hip_key_stream_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
@@ -713,7 +739,17 @@ def city64_batch_host(keys, out=None, device: int = 0):
 
 
 def city64_var_batch_host(data, offsets, out=None, device: int = 0):
+    """Host-resident variable-length keys: data uint8 [nbytes], offsets [n+1]
+    (uint64, or int64 with no negative entry -- numpy arrays and CPU tensors
+    alike, viewed as uint64 without a copy so pinned buffers stay pinned)."""
     _host_arr(data, "data", np.uint8)
+    if isinstance(offsets, np.ndarray) and offsets.dtype == np.int64:
+        if offsets.size and int(offsets.min()) < 0:
+            raise ValueError("offsets must not be negative")
+        offsets = offsets.view(np.uint64)
+    elif not isinstance(offsets, np.ndarray) and str(getattr(offsets, "dtype", "")) == "torch.int64":
+        if offsets.numel() and int(offsets.min()) < 0:
+            raise ValueError("offsets must not be negative")
     offsets = _host_arr(offsets, "offsets", np.uint64)
     n = offsets.size - 1 if isinstance(offsets, np.ndarray) else offsets.numel() - 1
     if n < 0:

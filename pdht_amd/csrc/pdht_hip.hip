@@ -627,7 +627,8 @@ static int host_fixed(const void *keys, size_t keylen, size_t n, size_t out_per_
 using namespace pdht;
 
 // ===================================================================== ABI ===
-PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.1 (gfx950, CityHash v1.0.x)"; }
+static_assert(PDHT_HIP_ABI_VERSION == 3, "bump the version string with the ABI");
+PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.3 (abi 3, gfx950, CityHash v1.0.x)"; }
 PDHT_API const char *pdht_hip_last_error(void) { return g_err; }
 PDHT_API const char *pdht_hip_last_kernel(void) { return g_kernel; }
 #ifdef PDHT_HIP_TUNING
@@ -1042,8 +1043,16 @@ struct BucketWs {
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
 static bool two_pass_keysize(size_t keysize) { return keysize == 8 || keysize == 16 || keysize == 32; }
+// Two-pass bucketing from this many ranks up (DESIGN.md §4.4: interleaved
+// A/B on 16M keys; at 1024 ranks one pass is 10 % faster for 8-B keys, equal
+// for 16-B keys, 30 % faster for 32-B keys; at 2048 ranks two passes are 1.3x
+// faster for 8-B keys and at 8192 ranks 2.1x).
+static u32 two_pass_min_ranks(size_t keysize) { return keysize == 8 ? 1536 : keysize == 16 ? 1025 : 2049; }
 // Sized for the smallest tile any scatter kernel uses, plus the two-pass
-// intermediate for the key sizes that can take that path.
+// intermediate when the batch can take that path: 8/16/32-B keys from
+// two_pass_min_ranks() up (the tuning build forces two passes at any nranks
+// and always reserves it).  16M x 8-B keys at 1024 ranks: 17 MB; from 1536
+// ranks + 192 MB.
 static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
   const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
@@ -1062,7 +1071,12 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
   off += round256((size_t)kTpMaxDigits * 8);
   w.tickets = reinterpret_cast<u32 *>(p + off);
   off += 256;
-  if (two_pass_keysize(keysize)) {
+#ifdef PDHT_HIP_TUNING
+  const bool two_pass = two_pass_keysize(keysize);
+#else
+  const bool two_pass = two_pass_keysize(keysize) && nranks >= two_pass_min_ranks(keysize);
+#endif
+  if (two_pass) {
     const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
     const u64 tp_chunks32 = (tp_tiles + kBucketChunk - 1) / kBucketChunk;
     const u64 tp_chunks = (tp_tiles + kTpChunkTiles - 1) / kTpChunkTiles;
@@ -1171,11 +1185,6 @@ static int launch_gather(const BucketArgs &a, const Out &out, u32 L, int lk, hip
 }
 #endif
 
-// Two-pass bucketing from this many ranks up (DESIGN.md §4.4: interleaved
-// A/B on 16M keys; at 1024 ranks one pass is 10 % faster for 8-B keys, equal
-// for 16-B keys, 30 % faster for 32-B keys; at 2048 ranks two passes are 1.3x
-// faster for 8-B keys and at 8192 ranks 2.1x).
-static u32 two_pass_min_ranks(size_t keysize) { return keysize == 8 ? 1536 : keysize == 16 ? 1025 : 2049; }
 
 template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false>
 static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,

@@ -439,6 +439,11 @@ def test_device_wrappers_validate_outputs(dev):
         P.bucket_records(k[:500].contiguous(), 16, out=rec)
     with pytest.raises(ValueError):
         P.city64_batch(k.cpu())
+    data = torch.zeros(100, dtype=torch.uint8, device=dev)
+    for bad in ([0, 50, 101], [60, 50, 100], [-8, 0, 10]):  # past the data, decreasing, negative
+        with pytest.raises(ValueError):
+            P.city64_var_batch(data, torch.tensor(bad, dtype=torch.int64, device=dev))
+    assert P.city64_var_batch(data, torch.tensor([0, 50, 100], dtype=torch.int64, device=dev)).numel() == 2
     s_other = torch.cuda.Stream(device=dev)
     assert P.city64_batch(k, stream=s_other).numel() == 1000  # a stream of the right device
 
@@ -765,6 +770,76 @@ def test_cfg1_place_1M_x64(dev, folds):
     from oracle import oracle as O
     assert f"{O.fold64(mb, 0):016x}" == f["mbits"]
     assert f"{O.fold64(rk.astype(np.uint64), 0):016x}" == pl["rank"]
+
+
+def test_cfg1_mpi_flavour_batches(dev, folds):
+    """a17, libmpipdht/hash.c:6-9 on the GPU: libpdht_hip_mpi.so's
+    pdht_hash_batch (host keys) and pdht_hash_batch_dev (device keys) over
+    cfg1's 1M x 64 B keys write mbits and rank = mbits % c->size and leave
+    every ptindex (and the nid/pid half of each ptl_process_t) untouched; the
+    mbits, rank and rankputs folds equal the reference's."""
+    import ctypes as C
+    f = folds["cfg1_pdht_hash_1M_x64"]
+    n = f["n"]
+    kd = device_keys(n, 64, dev=dev)
+    kh = kd.cpu().numpy()
+    L = P.mpi_lib()
+    SENT = 0xA5A5A5A5
+    for pl in f["placements"]:
+        t = P._PdhtT()
+        L.pdht_hip_table_init(C.byref(t), 64, pl["nptes"])
+        C.c_int.in_dll(L, "pdht_hip_shim_nranks").value = pl["nranks"]
+        # host batch: ptl_process_t[] ranks (stride 8)
+        mb = np.empty(n, np.uint64)
+        pt = np.full(n, SENT, np.uint32)
+        rk = np.full(2 * n, SENT, np.uint32)
+        assert L.pdht_hash_batch(C.byref(t), kh.ctypes.data, n, mb.ctypes.data, pt.ctypes.data,
+                                 rk.ctypes.data, 0) == 0, L.pdht_hip_last_error()
+        r = rk[0::2]
+        assert (pt == SENT).all() and (rk[1::2] == SENT).all()
+        assert (r.astype(np.uint64) == mb % np.uint64(pl["nranks"])).all()
+        from oracle import oracle as O
+        assert f"{O.fold64(mb, 0):016x}" == f["mbits"]
+        assert f"{O.fold64(r.astype(np.uint64), 0):016x}" == pl["rank"]
+        # device batch, with the rankputs histogram
+        mbd = torch.empty(n, dtype=torch.int64, device=dev)
+        sent32 = SENT - (1 << 32)  # the same bits as an int32
+        ptd = torch.full((n,), sent32, dtype=torch.int32, device=dev)
+        rkd = torch.full((2 * n,), sent32, dtype=torch.int32, device=dev)
+        hist = torch.zeros(pl["nranks"], dtype=torch.int64, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        assert L.pdht_hash_batch_dev(C.byref(t), kd.data_ptr(), n, mbd.data_ptr(), ptd.data_ptr(),
+                                     rkd.data_ptr(), hist.data_ptr(), s) == 0, L.pdht_hip_last_error()
+        torch.cuda.synchronize()
+        assert bool((ptd == sent32).all().item())
+        rr = rkd.view(n, 2)
+        assert bool((rr[:, 1] == sent32).all().item())
+        assert f"{gpu_fold(mbd):016x}" == f["mbits"]
+        assert f"{gpu_fold(rr[:, 0].to(torch.int64) & 0xFFFFFFFF):016x}" == pl["rank"]
+        assert f"{gpu_fold(hist):016x}" == pl["hist"]
+
+
+@pytest.mark.parametrize("L", [8, 16, 64])
+def test_place_batch_without_ptindex(dev, oracle, folds, L):
+    """place_batch(..., ptindex=False): the fused kernel with a NULL ptindex
+    (the libmpipdht placement) writes mbits, rank and the histogram only."""
+    if L == 64:
+        f = folds["cfg1_pdht_hash_1M_x64"]
+        kd = device_keys(f["n"], 64, dev=dev)
+        for pl in f["placements"]:
+            hist = torch.zeros(pl["nranks"], dtype=torch.int64, device=dev)
+            mb, pt, rk = P.place_batch(kd, pl["nptes"], pl["nranks"], ptindex=False, hist=hist)
+            assert pt is None
+            assert f"{gpu_fold(mb):016x}" == f["mbits"]
+            assert f"{gpu_fold(rk.to(torch.int64) & 0xFFFFFFFF):016x}" == pl["rank"]
+            assert f"{gpu_fold(hist):016x}" == pl["hist"]
+        return
+    rng = np.random.default_rng(L + 99)
+    k = rng.integers(0, 256, (300_001, L), dtype=np.uint8)
+    for nranks in (1, 7, 1000):
+        mb, pt, rk = P.place_batch(to_dev(k, dev), 3, nranks, ptindex=False)
+        m2, _, r2 = oracle.pdht_hash_fixed(k, 3, nranks)
+        assert pt is None and (u64(mb) == m2).all() and (rk.cpu().numpy().view(np.uint32) == r2).all()
 
 
 def test_batches_capture_in_hip_graph(dev, oracle):

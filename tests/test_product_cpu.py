@@ -218,9 +218,27 @@ def test_host_wrappers_reject_bad_buffers():
         P.city64_var_batch_host(data, np.array([0, 50, 101], np.uint64))
     with pytest.raises(ValueError):
         P.city64_var_batch_host(data, np.array([0, 50, 100], np.uint64), out=np.empty(1, np.uint64))
+    with pytest.raises(ValueError):  # int64 offsets are accepted, negative ones are not
+        P.city64_var_batch_host(data, np.array([0, -1, 100], np.int64))
     import torch
     with pytest.raises(ValueError):
+        P.city64_var_batch_host(data, torch.tensor([0, -1, 100], dtype=torch.int64))
+    with pytest.raises(ValueError):
         P.city64_batch_host(torch.zeros((10, 64), dtype=torch.uint8)[:, :32])
+
+
+def test_bucket_workspace_small_at_low_rank_counts():
+    """The two-pass intermediate (n x (keysize + 4) B) is reserved only at
+    the rank counts that take the two-pass sort."""
+    n = 16 << 20
+    for L, thr in ((8, 1536), (16, 1025), (32, 2049)):
+        small = P.bucket_workspace_bytes(n, L, 1024 if L != 16 else 1000)
+        assert small < 64 << 20, (L, small)
+        assert P.bucket_workspace_bytes(n, L, thr) >= small + n * (L + 4)
+        assert P.bucket_workspace_bytes(n, L, thr - 1) < n * (L + 4)
+    assert P.bucket_workspace_bytes(n, 8, 7) < 1 << 20
+    assert P.bucket_workspace_bytes(n, 13, 8192) < n * 17  # generic lengths never take two passes
+    assert b"abi 3" in P.lib().pdht_hip_version()
 
 
 def test_device_wrappers_reject_cpu_tensors():
