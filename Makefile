@@ -23,28 +23,29 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
 CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
 HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/bucket.h \
+           pdht_amd/csrc/runtime.h pdht_amd/csrc/launch.h pdht_amd/csrc/pdht_hip_tuning.h \
            include/pdht_hip.h include/pdht_city.h
 SHIM_HDR := include/pdht_hash.h include/pdht_hip.h include/pdht_city.h
-OBJ     := $(LIBDIR)/pdht_hip.o $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash.o
-OBJ_MPI := $(LIBDIR)/pdht_hip.o $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash_mpi.o
-OBJ_TUN := $(LIBDIR)/pdht_hip_tuning.o $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash.o
+# the C-ABI in translation units that build in parallel (make -j)
+HIP_UNITS := pdht_hip pdht_fixed64 pdht_fixed128 pdht_var pdht_host pdht_bucket
+OBJ_ENG := $(HIP_UNITS:%=$(LIBDIR)/%.o) $(LIBDIR)/city_host.o
+OBJ_TUN_ENG := $(HIP_UNITS:%=$(LIBDIR)/%.tun.o) $(LIBDIR)/city_host.o
+OBJ     := $(OBJ_ENG) $(LIBDIR)/pdht_hash.o
+OBJ_MPI := $(OBJ_ENG) $(LIBDIR)/pdht_hash_mpi.o
+OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
 
 .PHONY: all product oracle clean asm
 all: product oracle
 
 product: $(LIB) $(LIB_MPI) $(LIB_TUN)
 
-$(LIBDIR)/pdht_hip.o: pdht_amd/csrc/pdht_hip.hip $(HIP_HDR)
+$(LIBDIR)/%.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIBDIR)/pdht_hip_tuning.o: pdht_amd/csrc/pdht_hip.hip $(HIP_HDR) pdht_amd/csrc/pdht_hip_tuning.h
+$(LIBDIR)/%.tun.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DPDHT_HIP_TUNING -c -o $@ $<
-
-$(LIBDIR)/city_host.o: pdht_amd/csrc/city_host.hip $(HIP_HDR)
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(LIBDIR)/pdht_hash.o: pdht_amd/host/pdht_hash.c $(SHIM_HDR)
 	@mkdir -p $(LIBDIR)
@@ -69,7 +70,7 @@ oracle:
 # ISA listing of the kernels (for register / instruction counts)
 asm:
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/pdht_hip.s pdht_amd/csrc/pdht_hip.hip
+	for u in $(HIP_UNITS); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/$$u.s pdht_amd/csrc/$$u.hip || exit 1; done
 
 clean:
 	rm -f $(LIBDIR)/*.o $(LIB) $(LIB_MPI) $(LIB_TUN)

@@ -1,0 +1,363 @@
+// launch.h -- kernel choice and launch of the hash paths:
+// fixed-length keys (launch_fixed), variable-length keys (launch_var).
+// Included by the translation units that instantiate them.
+#pragma once
+#include "runtime.h"
+
+namespace pdht {
+
+constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wave (12 KiB)
+// Kernel tags (pdht_hip_last_kernel): the kernel and its launch shape, so a
+// profile taken of one shape (profiles/traffic_*.json) is never attributed to
+// another.
+
+// Packed 8/16/32-byte keys: each lane loads its own key (lane-adjacent rows,
+// so 8- and 16-byte keys are fully coalesced), U keys in flight per lane.
+// tools/placebench.py (interleaved A/B, r01): 8-B keys with non-temporal
+// stores (+26 % on fused placement), 16-B keys with non-temporal loads and
+// stores (+6-11 %).
+template <class Algo, class Sink>
+static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Sink sink,
+                         hipStream_t st, int dev, u64 blocks) {
+  typedef typename NtSink<Sink>::type SinkNt;
+  const SinkNt snt = NtSink<Sink>::make(sink);
+  if constexpr (std::is_same<Sink, SinkPlace>::value) {
+    // With a histogram: 1024-thread workgroups, 2 per CU.  Every workgroup
+    // flushes its LDS bins with one device-scope atomic per bin, and those
+    // run at the memory-side atomic rate (~1.3 TB/s of added bytes): 2048
+    // workgroups x 1024 bins x 8 B took ~16 us of an 85-us launch; a quarter
+    // as many workgroups measured +24 % (8-B keys) and +29 % (16-B keys) on
+    // 16M keys, 1024 ranks (tools/placebench.py, r01).
+    // (r02, tools/abbench.py place8_*: 8-B keys stream best at ONE such
+    // workgroup per CU -- 0.80 of the roofline against 0.74 at two, half the
+    // flushes again; 16-B keys stay at two)
+    if (sink.hist && keylen == 8) {
+      g_kernel = "k_fixed_direct<8,4,nt-store,1024>@1";
+      k_fixed_direct<8, 4, Algo, SinkNt, false, 1024>
+          <<<grid_for((blocks + 15) / 16, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
+      return;
+    }
+    if (sink.hist && keylen == 16) {
+      g_kernel = "k_fixed_direct<16,2,nt,1024>@2";
+      k_fixed_direct<16, 2, Algo, SinkNt, true, 1024>
+          <<<grid_for((blocks + 7) / 8, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+      return;
+    }
+  }
+  if (keylen == 8) {
+    g_kernel = "k_fixed_direct<8,4,nt-store>@8";
+    k_fixed_direct<8, 4, Algo, SinkNt, false><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(
+        k, n, algo, snt);
+  } else if (keylen == 16) {
+    g_kernel = "k_fixed_direct<16,2,nt>@8";
+    k_fixed_direct<16, 2, Algo, SinkNt, true><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(
+        k, n, algo, snt);
+  } else {
+    g_kernel = "k_fixed_direct<32,2>@8";
+    k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                            sink);
+  }
+}
+
+template <class Sink>
+static bool sink_has_hist(const Sink &s) {
+  if constexpr (std::is_same<Sink, SinkPlace>::value) return s.hist != nullptr;
+  return false;
+}
+
+// Fixed-length keys: the register-direct / LDS-transposed kernels for the
+// specialised lengths when the layout allows them, else the window kernel
+// (a 64-key tile fits 12 or 16 KiB of LDS), else per-lane global reads.
+template <class Algo, class Sink>
+static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo,
+                        Sink sink, hipStream_t st) {
+  if (n == 0) return 0;
+  if (!keys && keylen) return fail("null key pointer%s", "");  // empty keys read nothing
+  if (stride < keylen) return fail("stride < keylen%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  const uint8_t *k = static_cast<const uint8_t *>(keys);
+  const bool packed = stride == keylen;
+  const bool al16 = ((uintptr_t)k & 15) == 0;
+  const bool al8 = ((uintptr_t)k & 7) == 0;
+  const u64 blocks = (n + kBlock - 1) / kBlock;
+  typedef typename NtSink<Sink>::type SinkNt;
+  const SinkNt sink_nt = NtSink<Sink>::make(sink);
+  // the CRC-table algorithms serve keys > 900 B only: window / global kernels
+  constexpr bool kShort = !HasCrcLds<Algo>::value;
+  if (kShort && packed && keylen == 64 && al16) {
+#ifdef PDHT_HIP_TUNING
+    if constexpr (kShort) {
+      if (tuning_variant() == 7) {  // one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
+        g_kernel = "k_fixed_xpose64<nt,d1>@4";
+        k_fixed_xpose64<Algo, SinkNt, true, 1><<<grid_for((n + 255) / 256, 4, dev), kBlock, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+      if (tuning_variant() == 80 || tuning_variant() == 81) {  // 1024-thread workgroups, 1 / 2 per CU
+        g_kernel = tuning_variant() == 80 ? "k_fixed_xpose64<nt,d2,1024>@1" : "k_fixed_xpose64<nt,d2,1024>@2";
+        k_fixed_xpose64<Algo, SinkNt, true, 2, 1024>
+            <<<grid_for((n + 1023) / 1024, tuning_variant() == 80 ? 1 : 2, dev), 1024, 0, st>>>(k, n, algo,
+                                                                                                sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+      if (tuning_variant() == 82) {  // the 256-thread shape whatever the histogram
+        g_kernel = "k_fixed_xpose64<nt,d2>@3";
+        k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+      if (tuning_variant() == 26) {  // plain digest stores (r01: 2-6 % slower)
+        g_kernel = "k_fixed_xpose64<nt-load,plain-store,d2>@3";
+        k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+            k, n, algo, sink);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+    }
+#endif
+    // measured fastest (tools/kbench.py): non-temporal loads
+    // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU.
+    // Placement with a histogram on up to 4M keys: 1024-thread workgroups, 1
+    // per CU -- every workgroup ends with one device-scope atomic per bin, and
+    // with few ranks those all hit one cache line: 768 flushing workgroups
+    // cost ~6 us of a 24-us launch on 1M keys (cfg1), 256 cost ~1 us
+    // (tools/abbench.py cfg1: 24.3 -> 18.3 us); on 16M keys the wide shape
+    // streams 3-5 % slower and the 256-thread one stays.
+    if constexpr (kShort) {
+      if (sink_has_hist(sink) && n <= (4u << 20)) {
+        g_kernel = "k_fixed_xpose64<nt,d2,1024>@1";
+        k_fixed_xpose64<Algo, SinkNt, true, 2, 1024><<<grid_for((n + 1023) / 1024, 1, dev), 1024, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+    }
+    g_kernel = "k_fixed_xpose64<nt,d2>@3";
+    if constexpr (kShort)
+      k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+          k, n, algo, sink_nt);
+  } else if (kShort && packed && (((keylen == 32 || keylen == 16) && al16) || (keylen == 8 && al8))) {
+    if constexpr (kShort) launch_small(keylen, k, n, algo, sink, st, dev, blocks);
+  } else {
+    const u64 tiles = (n + 63) / 64;
+    const u64 tile_bytes = 63 * (u64)stride + keylen + 16;  // a 64-key tile + alignment slack
+    if (tile_bytes > 16384) {
+      // keys too long for a 64-key window: per-lane global reads (r01: an
+      // LDS chunk-streaming kernel measured 0.36-0.47 of peak against this
+      // kernel's 0.50-0.62 on 256 B - 8 KiB keys)
+      // 2 WG/CU: the per-lane walks of 64 keys touch 64 lines per wave
+      // instruction, and fewer waves keep more of those lines in L2 for the
+      // next 16-B pieces (r02, tools/abbench.py long64: 0.575 at 2 WG/CU
+      // against 0.535 at 8); the CRC path (LDS tables) is indifferent and
+      // keeps 8.
+      constexpr int kPerCu = kShort ? 2 : 8;
+      if (al16 && stride % 16 == 0) {
+#ifdef PDHT_HIP_TUNING
+        if (tuning_variant() == 93) {  // CRC-256 blocks as whole lines
+          g_kernel = "k_global<fixed,a16,lines>";
+          k_global<false, Algo, SinkNt, true, 3><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+        if (tuning_variant() == 98) {  // + CityHash128's shifted loop on line spans
+          g_kernel = "k_global<fixed,a16,lines16>";
+          k_global<false, Algo, SinkNt, true, 7><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+        if (tuning_variant() == 95 || tuning_variant() == 97) {  // 128-B spans (97: one carry array)
+          g_kernel = tuning_variant() == 95 ? "k_global<fixed,a16,pairs>" : "k_global<fixed,a16,lines16,1carry>";
+          if (tuning_variant() == 97)
+            k_global<false, Algo, SinkNt, true, 6><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          else
+            k_global<false, Algo, SinkNt, true, 4><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+        if (tuning_variant() == 96) {  // r02 before the line spans: 240-B / 64-B spans as the algorithm reads them
+          g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
+          k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+        if (tuning_variant() == 91 || tuning_variant() == 92) {  // nt span loads (all / all but the last line)
+          g_kernel = tuning_variant() == 91 ? "k_global<fixed,a16,nt>" : "k_global<fixed,a16,nt-head>";
+          if (tuning_variant() == 91)
+            k_global<false, Algo, SinkNt, true, 1><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          else
+            k_global<false, Algo, SinkNt, true, 2><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+#endif
+        g_kernel = kShort ? "k_global<fixed,a16,lines>@2" : "k_global<fixed,a16,lines>@8";
+        k_global<false, Algo, SinkNt, true, kLongLines><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+      } else {
+        g_kernel = kShort ? "k_global<fixed>@2" : "k_global<fixed>@8";
+        k_global<false, Algo, SinkNt><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+      }
+    } else if (tile_bytes > kWinBytes) {
+      g_kernel = "k_window<fixed,nt,16K>@2";
+      k_window<16384, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 2, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+    } else {  // (10224 B at 4 WG/CU measured 2-4 % slower for fixed keys: longbench r01)
+      g_kernel = "k_window<fixed,nt,12K>@3";
+      k_window<kWinBytes, false, Algo, SinkNt, 2><<<grid_for((tiles + 3) / 4, 3, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// Length-sorted window kernel (k_window_sorted): W waves per workgroup,
+// PER_CU workgroups per CU; the window takes what the CU's 160 KiB leave
+// after the sort tables (10 B per key), the histogram and the CRC tables.
+template <class Algo>
+constexpr int crc_lds_bytes() {
+  if constexpr (HasCrcLds<Algo>::value)
+    return (int)(Algo::Slices::kWords * 4);
+  else
+    return 0;
+}
+template <int W, int PER_CU, class Algo, class Sink>
+constexpr int sorted_winb() {
+  constexpr int crc = crc_lds_bytes<Algo>();
+  constexpr int fixed = 64 * W * 10 + W * (int)kSortBins * 4 + 16 + 4 * (int)Sink::kHist + crc + 64;
+  return (163840 / PER_CU - fixed) / 16 * 16;
+}
+template <int W, int PER_CU, class Algo, class Sink>
+static void launch_sorted(const uint8_t *b, const u64 *offsets, u64 obase, size_t n, Algo algo, Sink sink,
+                          hipStream_t st, int dev, const char *tag) {
+  constexpr int WINB = sorted_winb<W, PER_CU, Algo, Sink>();
+  g_kernel = tag;
+  const u64 tiles = (n + 64 * W - 1) / (64 * W);
+  k_window_sorted<W, WINB, Algo, Sink, 2><<<grid_for(tiles, PER_CU, dev), 64 * W, 0, st>>>(b, offsets, obase, n,
+                                                                                         algo, sink);
+}
+
+// Variable-length keys.  `nbytes` = key bytes the batch spans
+// (offsets[n] - offsets[0]; 0 = unknown) sizes the LDS window for the mean
+// key length (tools/varbench.py, r01): mean <= 160 B (cfg3's 16..256 mix,
+// mean 136) -> 10224 B per wave at 4 workgroups/CU; longer -> 16 KiB at 2.
+// (Per-lane global reads measured slower than the 16 KiB window even at
+// 1-3 KiB keys: the window's DMA pulls the lines into L2 for the keys that
+// overflow it.)
+template <class Algo, class Sink>
+static int launch_var(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
+                      Sink sink, hipStream_t st) {
+  if (n == 0) return 0;
+  if (!bytes || !offsets) return fail("null bytes/offsets pointer%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  const uint8_t *b = static_cast<const uint8_t *>(bytes);
+  typedef typename NtSink<Sink>::type SinkNt;
+  const SinkNt sink_nt = NtSink<Sink>::make(sink);
+  const u64 wb = ((n + 63) / 64 + 3) / 4;  // blocks of 4 wave-tiles
+  bool wide = nbytes / n > 160;
+#ifdef PDHT_HIP_TUNING
+  if (tuning_variant() == 12) wide = false;
+  if (tuning_variant() == 13) wide = true;
+  // 100-105: the length-sorted window kernel, W waves per workgroup @ per CU
+  // (nt = non-temporal digest stores, else plain)
+  switch (tuning_variant()) {
+    case 100: launch_sorted<8, 2>(b, offsets, obase, n, algo, sink_nt, st, dev, "k_window_sorted<8,nt>@2"); break;
+    case 101: launch_sorted<8, 2>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<8>@2"); break;
+    case 102: launch_sorted<4, 3>(b, offsets, obase, n, algo, sink_nt, st, dev, "k_window_sorted<4,nt>@3"); break;
+    case 103: launch_sorted<4, 3>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<4>@3"); break;
+    case 104: launch_sorted<4, 4>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<4>@4"); break;
+    case 105: launch_sorted<16, 1>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<16>@1"); break;
+    default: break;
+  }
+  if constexpr (BufStore<Sink>::kOk) {
+    if (tuning_variant() == 106 || tuning_variant() == 107) {  // next window in VGPRs (106: nt stores)
+      g_kernel = tuning_variant() == 106 ? "k_window_pf<10K,nt>@4" : "k_window_pf<10K>@4";
+      if (tuning_variant() == 106)
+        k_window_pf<10240, Algo, SinkNt><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                  sink_nt);
+      else
+        k_window_pf<10240, Algo, Sink><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo, sink);
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+  }
+  if (tuning_variant() >= 100 && tuning_variant() <= 105) {
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (tuning_variant() == 46) {  // windows start on a 128-B line
+    g_kernel = "k_window<var,nt,10224,a128>@4";
+    k_window<10224, true, Algo, SinkNt, 2, 128><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0,
+                                                                                       n, algo, sink_nt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (tuning_variant() >= 23 && tuning_variant() <= 25) {  // double-buffered windows
+    if (tuning_variant() == 23) {
+      g_kernel = "k_window_db<10224>@2";
+      k_window_db<10224, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                 sink_nt);
+    } else if (tuning_variant() == 24) {
+      g_kernel = "k_window_db<6656>@3";
+      k_window_db<6656, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                sink_nt);
+    } else {
+      g_kernel = "k_window_db<8192>@2";
+      k_window_db<8192, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                sink_nt);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (tuning_variant() == 48 || tuning_variant() == 49) {  // next window prefetched in VGPRs (48: nt loads)
+    g_kernel = tuning_variant() == 48 ? "k_window_rp<10224,nt>@4" : "k_window_rp<10224>@4";
+    if (tuning_variant() == 48)
+      k_window_rp<10224, Algo, SinkNt, true><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                    sink_nt);
+    else
+      k_window_rp<10224, Algo, SinkNt, false><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                     sink_nt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (tuning_variant() == 30 || tuning_variant() == 31) {  // offsets prefetched one tile ahead
+    if (tuning_variant() == 31 || wide) {
+      g_kernel = "k_window_var<16K>@2";
+      k_window_var<16384, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                  sink_nt);
+    } else {
+      g_kernel = "k_window_var<10224>@4";
+      k_window_var<10224, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                  sink_nt);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+#endif
+  if (wide) {
+    g_kernel = "k_window<var,nt,16K>@2";
+    k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,
+                                                                                    algo, sink_nt);
+  } else {
+    g_kernel = "k_window<var,nt,10224>@4";
+    k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,
+                                                                                    algo, sink_nt);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+}  // namespace pdht

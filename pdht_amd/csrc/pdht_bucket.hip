@@ -1,0 +1,479 @@
+// pdht_bucket.hip -- destination bucketing (include/pdht_hip.h
+// pdht_bucket_batch_dev / pdht_bucket_records_dev; kernels in bucket.h).
+#include "bucket.h"
+#include "runtime.h"
+
+// ------------------------------------------------- destination bucketing ---
+namespace pdht {
+struct BucketWs {
+  u32 *counts, *chunks;
+  u64 *totals, *base, *fbase;
+  u32 *tickets;  // [8] per-XCD tile tickets of the dynamic scatter
+  // two-pass sort (8/16/32-B keys): fine-bucket counts per tile and per
+  // 32-tile chunk, fine totals, rank counts per count-chunk, and the
+  // intermediate ([n][keysize] key rows + [n] original indices)
+  u32 *countsF, *chunksF, *chunkcnt;
+  u64 *totalsF;
+  uint8_t *ikeys;
+  u32 *iidx;
+  size_t bytes;
+};
+static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
+static bool two_pass_keysize(size_t keysize) { return keysize == 8 || keysize == 16 || keysize == 32; }
+// Two-pass bucketing from this many ranks up (interleaved
+// A/B on 16M keys; at 1024 ranks one pass is 10 % faster for 8-B keys, equal
+// for 16-B keys, 30 % faster for 32-B keys; at 2048 ranks two passes are 1.3x
+// faster for 8-B keys and at 8192 ranks 2.1x).
+static u32 two_pass_min_ranks(size_t keysize) { return keysize == 8 ? 1536 : keysize == 16 ? 1025 : 2049; }
+// Sized for the smallest tile any scatter kernel uses, plus the two-pass
+// intermediate when the batch can take that path: 8/16/32-B keys from
+// two_pass_min_ranks() up (the tuning build forces two passes at any nranks
+// and always reserves it).  16M x 8-B keys at 1024 ranks: 17 MB; from 1536
+// ranks + 192 MB.
+static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
+  const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
+  const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
+  BucketWs w{};
+  uint8_t *p = static_cast<uint8_t *>(ws);
+  size_t off = 0;
+  w.counts = reinterpret_cast<u32 *>(p + off);
+  off += round256((size_t)nranks * ntiles * 4);
+  w.chunks = reinterpret_cast<u32 *>(p + off);
+  off += round256((size_t)nranks * nchunks * 4);
+  w.totals = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)nranks * 8);
+  w.base = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)nranks * 8);
+  w.fbase = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)kTpMaxDigits * 8);
+  w.tickets = reinterpret_cast<u32 *>(p + off);
+  off += 256;
+#ifdef PDHT_HIP_TUNING
+  const bool two_pass = two_pass_keysize(keysize);
+#else
+  const bool two_pass = two_pass_keysize(keysize) && nranks >= two_pass_min_ranks(keysize);
+#endif
+  if (two_pass) {
+    const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
+    const u64 tp_chunks32 = (tp_tiles + kBucketChunk - 1) / kBucketChunk;
+    const u64 tp_chunks = (tp_tiles + kTpChunkTiles - 1) / kTpChunkTiles;
+    w.countsF = reinterpret_cast<u32 *>(p + off);
+    off += round256((size_t)tp_tiles * kTpMaxDigits * 4);
+    w.chunksF = reinterpret_cast<u32 *>(p + off);
+    off += round256((size_t)tp_chunks32 * kTpMaxDigits * 4);
+    w.totalsF = reinterpret_cast<u64 *>(p + off);
+    off += round256((size_t)kTpMaxDigits * 8);
+    w.chunkcnt = reinterpret_cast<u32 *>(p + off);
+    off += round256((size_t)tp_chunks * nranks * 4);
+    w.ikeys = p + off;
+    off += round256(n * keysize);
+    w.iidx = reinterpret_cast<u32 *>(p + off);
+    off += round256(n * 4);
+  }
+  w.bytes = off;
+  return w;
+}
+
+static int set_lds(const void *fn, size_t bytes) {
+  if (bytes > 65536)
+    HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return 0;
+}
+
+struct BucketArgs {
+  const uint8_t *k;
+  u64 n;
+  FastMod rk;
+  u32 nranks, nbits;
+  TileStarts ts;
+  u64 ntiles;
+};
+
+template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL, bool DYN = false, int OB = 0>
+static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev, u32 *tickets = nullptr) {
+  static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
+                                       "k_bucket_scatter_staged<32B>"};
+  static const char *const pnames[3] = {"k_bucket_scatter_staged<8B,u16>", "k_bucket_scatter_staged<16B,u16>",
+                                        "k_bucket_scatter_staged<32B,u16>"};
+  static const char *const onames[3] = {"k_bucket_scatter_staged<8B,own>", "k_bucket_scatter_staged<16B,own>",
+                                        "k_bucket_scatter_staged<32B,own>"};
+  static const char *const o8names[3] = {"k_bucket_scatter_staged<8B,own,8x16>",
+                                         "k_bucket_scatter_staged<16B,own,8x16>",
+                                         "k_bucket_scatter_staged<32B,own,8x16>"};
+  g_kernel = (OB ? (W == 8 ? o8names : onames) : PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK, OB);
+  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN, OB>;
+  if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
+  const int per_cu = bytes <= 53 * 1024 ? 3 : bytes <= 80 * 1024 ? 2 : 1;
+  unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
+  if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
+  // (DYN: 8 XCD groups need a grid that is a multiple of 8; small grids use
+  // the static order)
+  if (DYN && g % 8 == 0)
+    fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, tickets);
+  else
+    k_bucket_scatter_staged<L, Out, W, KPL, PACK, false, OB>
+        <<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, nullptr);
+  return 0;
+}
+
+#ifdef PDHT_HIP_TUNING
+template <int W, int L, int KPL, class Out>
+static int launch_reg(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
+  static const char *const names[3] = {"k_bucket_scatter_reg<8B>", "k_bucket_scatter_reg<16B>",
+                                       "k_bucket_scatter_reg<32B>"};
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  const size_t bytes = (size_t)W * a.nranks * 4;
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_reg<W, L, KPL, Out>), bytes)) return rc;
+  k_bucket_scatter_reg<W, L, KPL, Out><<<grid_for(a.ntiles, 2, dev), W * 64, bytes, st>>>(
+      a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+  return 0;
+}
+
+#endif
+
+template <int W, class Out>
+static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st, int dev) {
+  g_kernel = W == 8 ? "k_bucket_scatter_wg<8>" : "k_bucket_scatter_wg<4>";
+  const size_t bytes = (size_t)W * a.nranks * 4;
+  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_wg<W, Out>), bytes)) return rc;
+  k_bucket_scatter_wg<W, Out><<<grid_for(a.ntiles, 4, dev), W * 64, bytes, st>>>(
+      a.k, L, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+  return 0;
+}
+
+#ifdef PDHT_HIP_TUNING
+template <int W, int KPL, class Out>
+static int launch_gather(const BucketArgs &a, const Out &out, u32 L, int lk, hipStream_t st, int dev) {
+  const size_t bytes = gather_lds_bytes(a.nranks, W, KPL);
+  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
+  auto go = [&](auto fn, const char *name) -> int {
+    g_kernel = name;
+    if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
+    unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
+    if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
+    fn<<<g, W * 64, bytes, st>>>(a.k, L, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+    return 0;
+  };
+  if (lk == 8) return go(&k_bucket_scatter_gather<8, Out, W, KPL>, "k_bucket_scatter_gather<8B>");
+  if (lk == 16) return go(&k_bucket_scatter_gather<16, Out, W, KPL>, "k_bucket_scatter_gather<16B>");
+  if (lk == 32) return go(&k_bucket_scatter_gather<32, Out, W, KPL>, "k_bucket_scatter_gather<32B>");
+  return go(&k_bucket_scatter_gather<0, Out, W, KPL>, "k_bucket_scatter_gather<any>");
+}
+#endif
+
+
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false>
+static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
+                           u32 *tickets) {
+  static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
+  constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;  // waves per SIMD
+  const size_t b1 = pass1_lds_bytes<W, KPL>(), b2 = pass2_lds_bytes<W, KPL>();
+  auto f1 = &k_bucket_pass1<L, W, KPL, WPE, DBG, DYN>;
+  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, DYN>;
+  auto f1s = &k_bucket_pass1<L, W, KPL, WPE, DBG, false>;
+  auto f2s = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, false>;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f1s), b1)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f2s), b2)) return rc;
+  const u64 cus = (u64)std::max(1, g_dev[dev].cus);
+  unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU);
+  if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
+  // (tickets need a grid that is a multiple of 8; small grids: static order)
+  if (DYN && g1 % 8 == 0)
+    f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp, tickets);
+  else
+    f1s<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp, nullptr);
+  unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
+  if (g2 >= 8) g2 &= ~7u;
+  if (DYN && g2 % 8 == 0)
+    f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out, tickets + 8);
+  else
+    f2s<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out, nullptr);
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  return 0;
+}
+
+template <int L, class Out>
+static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
+                               u32 *tickets) {
+#ifdef PDHT_HIP_TUNING
+  // 73-76: sub-tile shape (waves x keys per lane) and workgroups per CU;
+  // 77: 73 with contiguous stores (timing-only, wrong results); 86: per-XCD
+  // tile tickets
+  switch (tuning_variant()) {
+    case 73: return launch_two_pass<L, Out, 4, 8, 4>(a, tp, out, st, dev, tickets);
+    case 74: return launch_two_pass<L, Out, 8, 4, 4>(a, tp, out, st, dev, tickets);
+    case 75: return launch_two_pass<L, Out, 4, 16, 2>(a, tp, out, st, dev, tickets);
+    case 76: return launch_two_pass<L, Out, 4, 4, 6>(a, tp, out, st, dev, tickets);
+    case 77: return launch_two_pass<L, Out, 4, 8, 4, 1>(a, tp, out, st, dev, tickets);  // timing-only
+    case 86: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, true>(a, tp, out, st, dev, tickets);
+    default: break;
+  }
+#endif
+  return launch_two_pass<L, Out>(a, tp, out, st, dev, tickets);
+}
+
+enum class BucketKernel { kGather, kStaged, kReg, kGeneric, kTwoPass };
+
+enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16, kOwner4x24 };
+template <class Out>
+static StagedShape staged_shape(size_t keysize, u32 nranks) {
+  if (nranks < 512) return StagedShape::kBallot4x16;
+  if (!std::is_same<Out, OutSoA>::value) {
+    // records: owner ranking pays for 16/32-B keys only (ab_records_*_shapes.log:
+    // 16-B at 1024 ranks 0.62 -> 0.56 ms, 32-B 1.29 -> 1.20); 8-B records
+    // lose 3 % with it
+    if (keysize != 8 && staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024)
+      return StagedShape::kOwner4x16;
+    return StagedShape::kBallot4x16;
+  }
+  if (keysize != 32 && staged_lds_bytes(nranks, 8, 16, false, 2) <= 160 * 1024) return StagedShape::kOwner8x16;
+  if (staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024) return StagedShape::kOwner4x16;
+  return StagedShape::kBallot4x16;
+}
+
+// Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
+// (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
+// out_al: alignment bits of the output key rows (0 when they are 8-B aligned
+// 8-B pieces, as in records).
+template <class Out>
+static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nranks, void *workspace,
+                       size_t workspace_bytes, const Out &out, uintptr_t out_al, uint64_t *bucket_offsets,
+                       hipStream_t st) {
+  if (nranks == 0) return fail("nranks must be > 0%s", "");
+  if (nranks > kBucketMaxRanks) return fail("bucketing supports up to 8192 ranks%s", "");
+  if (n >= (1ull << 32)) return fail("bucketing: n must be < 2^32 per call%s", "");
+  if (!bucket_offsets) return fail("bucket_offsets must not be NULL%s", "");
+  if (n && (!keys || keysize == 0)) return fail("null keys or zero keysize%s", "");
+  const BucketWs w = bucket_layout(workspace, n, keysize, nranks);
+  if (!workspace || workspace_bytes < w.bytes) return fail("workspace too small%s", "");
+  int dev;
+  if (int rc = current_device(&dev)) return rc;
+  // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter up to
+  // 2048 ranks, register scatter above; other lengths -> generic.
+  const uintptr_t al = (uintptr_t)keys | out_al;
+  const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
+  // (two_pass_min_ranks <= kStagedMaxRanks + 1: the staged scatter covers
+  // every nranks below the two-pass threshold)
+  BucketKernel kind = !fixed                                ? BucketKernel::kGeneric
+                      : nranks >= two_pass_min_ranks(keysize) ? BucketKernel::kTwoPass
+                                                              : BucketKernel::kStaged;
+  int ga_w = kGaW, ga_kpl = kGaKPL;
+#ifdef PDHT_HIP_TUNING
+  // 21 generic, 22 register scatter; 54 the gather scatter (16384-key tiles,
+  // keys gathered back from L2 and re-hashed), 52 / 53 it with 8192-key
+  // tiles (4 waves x 32 / 8 waves x 16 keys per lane); 55-57 its timing-only
+  // builds; 58 producer/consumer scatter; 50 staged with u16 run tables.
+  // All measured slower than the staged scatter.
+  // 70: one pass (staged / register scatter) at any nranks; 71: two passes
+  // at any nranks >= 2.
+  if (tuning_variant() == 70 && kind == BucketKernel::kTwoPass)
+    kind = nranks > kStagedMaxRanks ? BucketKernel::kReg : BucketKernel::kStaged;
+  if (tuning_variant() == 71 && fixed && nranks >= 2) kind = BucketKernel::kTwoPass;
+  if (tuning_variant() == 21) kind = BucketKernel::kGeneric;
+  if (tuning_variant() == 22 && fixed) kind = BucketKernel::kReg;
+  if (tuning_variant() >= 52 && tuning_variant() <= 58 && nranks <= kStagedMaxRanks) kind = BucketKernel::kGather;
+  if (tuning_variant() == 52) ga_w = 4;
+  if (tuning_variant() == 53) ga_kpl = 16;
+#endif
+  // Staged scatter shape (tools/abbench.py): owner-table
+  // ranking for array outputs from 512 ranks; with it, 8 waves x 16 keys per
+  // lane (8192-key tiles, 1 WG/CU) for 8/16-B keys while the LDS holds
+  // (8-B keys at 1024 ranks 0.274 -> 0.261 ms, 16-B 0.443 -> 0.405; 32-B
+  // keys lose 11 % and keep 4 x 16); else 4 x 16 while two workgroups fit a
+  // CU (<= 1462 ranks); ballots below 512 ranks and for records.
+  StagedShape shape = staged_shape<Out>(keysize, nranks);
+#ifdef PDHT_HIP_TUNING
+  if (tuning_variant() == 83) shape = StagedShape::kOwner8x16;
+  if (tuning_variant() == 87) shape = StagedShape::kOwner4x16;
+  if (tuning_variant() == 84 && keysize == 8) shape = StagedShape::kOwner4x24;
+  if (tuning_variant() == 85 || tuning_variant() == 89) shape = StagedShape::kBallot4x16;
+#endif
+  const u64 st_tile = shape == StagedShape::kOwner8x16 ? 8192 : shape == StagedShape::kOwner4x24 ? 6144 : kStTile;
+  const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
+  const int reg_kpl = keysize == 32 ? 8 : 16;
+  const u64 tile = kind == BucketKernel::kGather     ? (u64)ga_w * ga_kpl * 64
+                   : kind == BucketKernel::kTwoPass ? kTpCountTile
+                   : kind == BucketKernel::kStaged   ? st_tile
+                   : kind == BucketKernel::kReg    ? (u64)waves * reg_kpl * 64
+                                                   : (u64)waves * kScatKPL * 64;
+  const u64 ntiles = (n + tile - 1) / tile;
+  const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
+  BucketArgs a{};
+  a.k = static_cast<const uint8_t *>(keys);
+  a.n = n;
+  a.rk = make_fastmod(nranks);
+  a.nranks = nranks;
+  while ((1u << a.nbits) < nranks) ++a.nbits;
+  a.ts = TileStarts{w.counts, w.chunks, w.base, nranks};
+  a.ntiles = ntiles;
+  const size_t hist_lds = (size_t)nranks * 4;
+  TwoPass tp{};
+  if (kind == BucketKernel::kTwoPass) {
+    tp.fbits = (a.nbits + 1) / 2;
+    tp.F = 1u << tp.fbits;
+    tp.C = (nranks + tp.F - 1) >> tp.fbits;
+    tp.cbits = a.nbits - tp.fbits;
+    tp.countsF = w.countsF;
+    tp.chunksF = w.chunksF;
+    tp.totalsF = w.totalsF;
+    tp.chunkcnt = w.chunkcnt;
+    tp.base = w.base;
+    tp.fbase = w.fbase;
+    tp.ikeys = w.ikeys;
+    tp.iidx = w.iidx;
+    tp.ntiles = ntiles;
+    tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
+    tp.SG = std::max<u64>(1, tp.F / kTpChunkTiles);  // ~4096 keys per segment
+    tp.nsegf = (tp.nchunks + tp.SG - 1) / tp.SG;
+    tp.nseg = (u64)tp.F * tp.nsegf;
+  }
+  if (ntiles && kind == BucketKernel::kTwoPass) {
+    const u64 nchunks32 = (ntiles + kBucketChunk - 1) / kBucketChunk;
+    const unsigned gc = (unsigned)std::min<u64>(tp.nchunks, (u64)std::max(1, g_dev[dev].cus) * 8);
+    if (keysize == 8)
+      k_bucket_count_tp<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
+                                                          ntiles);
+    else if (keysize == 16)
+      k_bucket_count_tp<16><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
+                                                           ntiles);
+    else
+      k_bucket_count_tp<32><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
+                                                           ntiles);
+    k_bucket_colscan<<<dim3((tp.F + 63) / 64, (unsigned)nchunks32), 64, 0, st>>>(w.countsF, ntiles, tp.F,
+                                                                                   w.chunksF);
+    k_bucket_chunkscan<<<(tp.F + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunksF, nchunks32, tp.F, w.totalsF);
+    k_bucket_chunkscan<<<(nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunkcnt, tp.nchunks, nranks,
+                                                                        w.totals);
+  } else if (ntiles) {
+    const unsigned gc = grid_for(ntiles, 8, dev);
+    if (fixed && keysize == 8)
+      k_bucket_count_reg<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
+    else if (fixed && keysize == 16)
+      k_bucket_count_reg<16><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
+    else if (fixed && keysize == 32)
+      k_bucket_count_reg<32><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
+    else
+      k_bucket_count<<<gc, kBlock, hist_lds, st>>>(a.k, (u32)keysize, n, a.rk, nranks, w.counts, ntiles,
+                                                   tile);
+    k_bucket_colscan<<<dim3((nranks + 63) / 64, (unsigned)nchunks), 64, 0, st>>>(w.counts, ntiles, nranks,
+                                                                                 w.chunks);
+    k_bucket_chunkscan<<<(nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunks, nchunks, nranks,
+                                                                        w.totals);
+  } else {
+    HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
+  }
+  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, tp.fbits, w.totalsF,
+                                            kind == BucketKernel::kTwoPass ? w.fbase : nullptr, w.tickets);
+  g_kernel = "k_bucket_base";
+  if (ntiles) {
+    int rc = 0;
+#ifdef PDHT_HIP_TUNING
+    const int lk = fixed ? (int)keysize : 0;
+    if (kind == BucketKernel::kGather && !(tuning_variant() >= 55 && tuning_variant() <= 58 && lk == 8)) {
+      if (ga_w == 8 && ga_kpl == 32)
+        rc = launch_gather<8, 32>(a, out, (u32)keysize, lk, st, dev);
+      else if (ga_w == 4)
+        rc = launch_gather<4, 32>(a, out, (u32)keysize, lk, st, dev);
+      else
+        rc = launch_gather<8, 16>(a, out, (u32)keysize, lk, st, dev);
+    } else if (kind == BucketKernel::kGather && lk == 8 && tuning_variant() == 58) {
+      // producer/consumer scatter: 8 + 8 waves, 16384-key tiles, 1 WG/CU
+      const size_t bytes = (size_t)8 * a.nranks * 4 + (size_t)2 * a.nranks * 4 + (size_t)2 * 16384 * 2;
+      auto fn = &k_bucket_scatter_pc<Out, 8, 32>;
+      g_kernel = "k_bucket_scatter_pc<8B>";
+      if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
+      unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus));
+      if (g >= 8) g &= ~7u;
+      fn<<<g, 1024, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+    } else if (kind == BucketKernel::kGather && ga_w == 8 && ga_kpl == 32 && lk == 8 &&
+               tuning_variant() >= 55 && tuning_variant() <= 57) {
+      // timing-only builds (wrong results): 55 no stores, 56 no gather, 57 no phase D
+      const size_t bytes = gather_lds_bytes(a.nranks, 8, 32);
+      const int v = tuning_variant();
+      auto fn = v == 55 ? &k_bucket_scatter_gather<8, Out, 8, 32, 32, 1>
+                : v == 56 ? &k_bucket_scatter_gather<8, Out, 8, 32, 32, 2>
+                          : &k_bucket_scatter_gather<8, Out, 8, 32, 32, 4>;
+      g_kernel = "k_bucket_scatter_gather<8B,timing-only>";
+      if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
+      unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * 2) & ~7u;
+      fn<<<g, 512, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
+    } else if (kind == BucketKernel::kStaged && tuning_variant() == 85)  // static tile order (r02 default before)
+      rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
+                           : launch_staged<32, Out>(a, out, st, dev);
+    else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
+      rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
+                           : launch_staged<32, Out, true>(a, out, st, dev);
+    else
+#endif
+    if (kind == BucketKernel::kTwoPass)
+      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev, w.tickets)
+                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev, w.tickets);
+    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner8x16)
+      rc = keysize == 8    ? launch_staged<8, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets);
+    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner4x16)
+      rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets);
+#ifdef PDHT_HIP_TUNING
+    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner4x24)  // slower (spills)
+      rc = launch_staged<8, Out, false, 4, 24, true, 2>(a, out, st, dev, w.tickets);
+#endif
+    else if (kind == BucketKernel::kStaged)  // per-XCD tile tickets
+      rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
+                           : launch_staged<32, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets);
+#ifdef PDHT_HIP_TUNING
+    else if (kind == BucketKernel::kReg)
+      rc = keysize == 8 ? (waves == 8 ? launch_reg<8, 8, 16>(a, out, st, dev) : launch_reg<4, 8, 16>(a, out, st, dev))
+           : keysize == 16
+               ? (waves == 8 ? launch_reg<8, 16, 16>(a, out, st, dev) : launch_reg<4, 16, 16>(a, out, st, dev))
+               : (waves == 8 ? launch_reg<8, 32, 8>(a, out, st, dev) : launch_reg<4, 32, 8>(a, out, st, dev));
+#endif
+    else
+      rc = waves == 8 ? launch_wg<8>(a, out, (u32)keysize, st, dev) : launch_wg<4>(a, out, (u32)keysize, st, dev);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+}  // namespace pdht
+
+using namespace pdht;
+
+
+PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks) {
+  return bucket_layout(nullptr, n, keysize, nranks).bytes;
+}
+
+PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
+                                   uint32_t nranks, void *workspace, size_t workspace_bytes,
+                                   void *keys_out, uint64_t *mbits_out, uint32_t *ptindex_out,
+                                   uint32_t *index_out, uint64_t *bucket_offsets,
+                                   pdht_hip_stream_t s) {
+  if (int rc = check_place(n, mbits_out, nptes, nranks, nullptr, 0)) return rc;
+  const OutSoA out{static_cast<uint8_t *>(keys_out), mbits_out, ptindex_out, index_out, make_fastmod(nptes),
+                   (u32)keysize};
+  return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, out, (uintptr_t)keys_out,
+                     bucket_offsets, ST(s));
+}
+
+PDHT_API size_t pdht_bucket_record_bytes(size_t keysize) { return 24 + ((keysize + 7) & ~(size_t)7); }
+
+PDHT_API int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n, uint32_t nranks,
+                                     uint32_t msg_type, uint32_t src_rank, uint32_t ht_index,
+                                     void *workspace, size_t workspace_bytes, void *records,
+                                     uint64_t *bucket_offsets, pdht_hip_stream_t s) {
+  if (n && !records) return fail("records must not be NULL%s", "");
+  if ((uintptr_t)records & 7) return fail("records must be 8-byte aligned%s", "");
+  const OutRec out{static_cast<uint8_t *>(records), (u64)pdht_bucket_record_bytes(keysize),
+                   (u64)msg_type | ((u64)src_rank << 32), ht_index, (u32)keysize};
+  return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, out, 0, bucket_offsets, ST(s));
+}

@@ -1,0 +1,70 @@
+// pdht_var.hip -- device-resident batches of variable-length (offset-indexed)
+// keys and their data-movement calibration (include/pdht_hip.h).
+#include "launch.h"
+
+using namespace pdht;
+
+PDHT_API int pdht_city64_batch_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                       size_t n, uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_var(bytes, nbytes, offsets, 0, n, AlgoCity64{}, Sink64{nullptr, out}, ST(s));
+}
+
+PDHT_API int pdht_city128_batch_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                        size_t n, uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  return launch_var(bytes, nbytes, offsets, 0, n, AlgoCity128{}, Sink128{nullptr, out}, ST(s));
+}
+
+PDHT_API int pdht_citycrc128_batch_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                           size_t n, uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+  // any key may exceed 900 B (CityHashCrc256 rounds): CRC-32C tables in LDS
+  return launch_var(bytes, nbytes, offsets, 0, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
+}
+
+// Variable-length counterpart: the default offset-indexed kernel's data
+// movement (window DMA, offsets, LDS reads of every key byte, digest stores)
+// with an XOR fold for the hash.
+PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const uint64_t *offsets,
+                                         size_t n, uint64_t *out, pdht_hip_stream_t s) {
+  if (n && !out) return fail("null out%s", "");
+#ifdef PDHT_HIP_TUNING
+  // data-movement calibrations of the window kernel (no LDS reads, digest =
+  // key length): 40 as shipped; 41 default-policy DMA; 42 plain stores;
+  // 43 as 40 at 3 WG/CU; 44 offsets prefetched (k_window_var)
+  const int v = tuning_variant();
+  if (v >= 40 && v <= 45) {
+    if (n == 0) return 0;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    const uint8_t *b = static_cast<const uint8_t *>(bytes);
+    const u64 wb = ((n + 63) / 64 + 3) / 4;
+    const Sink64T<true> snt{nullptr, out};
+    const Sink64 spl{nullptr, out};
+    hipStream_t st = ST(s);
+    g_kernel = "k_window<var,calib>";
+    if (v == 40)
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else if (v == 41)
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 0><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else if (v == 42)
+      k_window<10224, true, AlgoLenOnly, Sink64, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, spl);
+    else if (v == 43)
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else if (v == 45)  // windows start on a 128-B line
+      k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2, 128><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
+    else
+      k_window_var<10224, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, 0, n, AlgoLenOnly{}, snt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+#endif
+  return launch_var(bytes, nbytes, offsets, 0, n, AlgoFoldVar{}, Sink64{nullptr, out}, ST(s));
+}

@@ -261,7 +261,10 @@ def test_var_golden_mixed(dev, golden, oracle):
 
 
 VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2",
-               48: "k_window_rp<10224,nt>@4", 49: "k_window_rp<10224>@4"}
+               48: "k_window_rp<10224,nt>@4", 49: "k_window_rp<10224>@4",
+               100: "k_window_sorted<8,nt>@2", 101: "k_window_sorted<8>@2", 102: "k_window_sorted<4,nt>@3",
+               103: "k_window_sorted<4>@3", 104: "k_window_sorted<4>@4", 105: "k_window_sorted<16>@1",
+               106: "k_window_pf<10K,nt>@4", 107: "k_window_pf<10K>@4"}
 
 
 def auto_var_kernel(total_bytes, n):
@@ -440,7 +443,7 @@ def test_device_wrappers_validate_outputs(dev):
     with pytest.raises(ValueError):
         P.city64_batch(k.cpu())
     data = torch.zeros(100, dtype=torch.uint8, device=dev)
-    for bad in ([0, 50, 101], [60, 50, 100], [-8, 0, 10]):  # past the data, decreasing, negative
+    for bad in ([0, 50, 101], [60, 70, 50], [-8, 0, 10]):  # past the data, end before start, negative
         with pytest.raises(ValueError):
             P.city64_var_batch(data, torch.tensor(bad, dtype=torch.int64, device=dev))
     assert P.city64_var_batch(data, torch.tensor([0, 50, 100], dtype=torch.int64, device=dev)).numel() == 2
@@ -713,7 +716,7 @@ def test_cfg4_crc128_16M_full_fold(dev, folds):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-@pytest.mark.parametrize("variant", [0, 13, 48])
+@pytest.mark.parametrize("variant", [0, 13, 48, 100, 101, 102, 103, 104, 105, 106, 107])
 def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     """8.7 GB of keys: offsets far past 2^31 and 2^32 (64-bit window math)."""
     f = folds["cfg3_city64_64M_mixed"]

@@ -96,8 +96,8 @@ def workload(name, dev):
     data = P.splitmix64_fill(SEED, 0, (total + 7) // 8, device=dev).view(torch.uint8)[:total]
     out = torch.empty(n, dtype=torch.int64, device=dev)
     if name == "cfg3fold":  # the window kernel's data movement, hash replaced (variant 40: no LDS reads)
-        return (lambda: P.key_stream_var(data, offs, out=out)), (lambda: out[:1].clone()), total + 16 * n
-    return (lambda: P.city64_var_batch(data, offs, out=out)), (lambda: out.clone()), total + 16 * n
+        return (lambda: P.key_stream_var(data, offs, out=out, check=False)), (lambda: out[:1].clone()), total + 16 * n
+    return (lambda: P.city64_var_batch(data, offs, out=out, check=False)), (lambda: out.clone()), total + 16 * n
 
 
 def main():

@@ -4,17 +4,25 @@
 #   tools/gpu_session.sh tests smoke bench bench_cfg3 ab_cfg2 prof_cfg2 pmc_cfg2 sq_long
 # Knobs (environment of the session script only, never read by the library):
 #   K=<pytest -k expr> for ktests; VARIANTS / PERCU for ab_*; PMCS for pmc_*.
+set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-PYT="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread"
+# heartbeat: every step has its own timeout, so a hung step is ended by that,
+# not by gpurun's silence limit (long bench / profile steps print at the end)
+( while sleep 50; do echo "[hb $(date +%T)]"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+PYT="python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread"
 for step in "$@"; do
+  echo "[step $step start $(date +%T)]"
   case $step in
     tests)   timeout -k 10 900 $PYT tests -m gpu > gpurun_out/gpu_tests.log 2>&1; rc=$?
+             grep -c PASSED gpurun_out/gpu_tests.log
              tail -4 gpurun_out/gpu_tests.log ;;
     ktests)  timeout -k 10 600 $PYT tests -m gpu -k "$K" > gpurun_out/gpu_ktests.log 2>&1; rc=$?
              tail -15 gpurun_out/gpu_ktests.log | cut -c1-300 ;;
-    smoke)   timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+    smoke)   timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log; rc=$?
              tail -1 gpurun_out/smoke.log ;;
     bench)   timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
              tail -1 gpurun_out/bench.log | cut -c1-600 ;;
@@ -37,6 +45,10 @@ for step in "$@"; do
     sq_*)    cfg=${step#sq_}
              timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sq_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/sq_$cfg.log 2>&1; rc=$?
              tail -3 gpurun_out/sq_$cfg.log | cut -c1-300 ;;
+    sqab_*)  w=${step#sqab_}
+             # SQ counters of the A/B harness's variants (one rocprofv3 pass; kernels told apart by name)
+             timeout -s KILL 200 rocprofv3 --pmc ${PMCS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS} --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sqab_$w" -o run --output-format csv -- python3 tools/abbench.py --work $w --variants ${VARIANTS:-0} --rounds 1 --reps 3 > gpurun_out/sqab_$w.log 2>&1; rc=$?
+             python3 tools/pmc_summary.py gpurun_out/sqab_$w/run_counter_collection.csv ;;
     torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-host > gpurun_out/torchrun1.log 2>&1; rc=$?
              tail -1 gpurun_out/torchrun1.log | cut -c1-600 ;;
     *) echo "unknown step $step"; rc=0 ;;
