@@ -727,11 +727,12 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
         data, offsets = O.mixed_keys(s_n)
         L = 0
         what = "the first 4M mixed 16..256B keys of the stream (offset-indexed)"
-    elif cfg in ("place", "bucket", "bucket8k", "exchange", "records", "xrecords"):
-        s_n, mode, nptes, nranks, L = 4 * M, 2, 3, 8192 if cfg == "bucket8k" else 1024, 8
+    elif cfg == "place":
+        s_n, mode, nptes, nranks, L = 4 * M, 2, 3, 1024, 8
         data = O.fixed_keys(s_n, 8)
-        what = (f"the first 4M x 8B keys, pdht_hash semantics (nptes 3, nranks {nranks})"
-                + ("; hashing and placement only, no bucketing" if cfg != "place" else ""))
+        what = f"the first 4M x 8B keys, pdht_hash semantics (nptes 3, nranks {nranks})"
+    elif cfg in ("bucket", "bucket8k", "exchange", "records", "xrecords"):
+        return cpu_bucket_baseline(cfg, budget_s, P, torch, O, cpus)
     else:
         return None
     try:
@@ -774,6 +775,60 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
                                outs=(d1, p1, r1))[0] for _ in range(5))
         res["cfg1_single_thread_pdht_hash_Gkeys_s"] = round(M / one / 1e9, 4)
     return res
+
+
+def cpu_bucket_baseline(cfg, budget_s, P, torch, O, cpus):
+    """f4's CPU baseline: destination bucketing on the host cores -- the
+    reference CityHash64 (oracle/_ref) per key, a count per rank and a stable
+    scatter by rank (the count-then-ship shape of
+    bench/Meraculous/buildUFXhashBinary.h:103-109, :255-279), with every
+    thread of the job's CPU share (oracle_time_bucket).  Outputs as the GPU's:
+    bucketed keys, mbits, ptindex and original index (records: the wire
+    records).  Best of 5 after >= 1 s of warm-up; the sample's bucketing is
+    compared with the GPU's bucketing of the same keys."""
+    thr = cpus["threads"]
+    s_n, L = 4 * M, 8
+    records = cfg in ("records", "xrecords")
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    nranks = {"bucket": 1024, "bucket8k": 8192, "records": 1024}.get(cfg, world)
+    keys = O.fixed_keys(s_n, L)
+    try:
+        fn, kind = O.cpu_fn("CityHash64")
+    except RuntimeError as e:
+        return {"error": str(e)}
+    bufs = O.BucketBufs(s_n, L, nranks, thr, records)
+
+    def run(reps):
+        return O.time_bucket(fn, keys, 3, nranks, threads=thr, reps=reps, records=records, bufs=bufs)[0]
+
+    run(1)
+    t_w, secs = 0.0, float("inf")
+    while t_w < 1.0:
+        dt = run(1)
+        t_w += dt
+        secs = min(secs, dt)
+    reps = max(1, int(budget_s / max(secs, 1e-6)))
+    best = min(run(reps) for _ in range(5))
+    # the GPU's bucketing of the same sample, compared field by field
+    kd = torch.from_numpy(keys).to(torch.device("cuda", torch.cuda.current_device()))
+    if records:
+        rec, offs = P.bucket_records(kd, nranks)
+        ok = bool((rec.cpu().numpy() == bufs.rec).all()) and bool((offs.cpu().numpy() == bufs.offsets.view(np.int64)).all())
+    else:
+        ko, mb, pt, ix, offs = P.bucket_batch(kd, 3, nranks)
+        ok = (bool((ko.cpu().numpy() == bufs.keys).all()) and bool((mb.cpu().numpy().view(np.uint64) == bufs.mbits).all())
+              and bool((pt.cpu().numpy().view(np.uint32) == bufs.pt).all())
+              and bool((ix.cpu().numpy().view(np.uint32) == bufs.idx).all())
+              and bool((offs.cpu().numpy() == bufs.offsets.view(np.int64)).all()))
+    form = "wire records" if records else "keys, mbits, ptindex and index arrays"
+    return {"value": round(s_n * reps / best / 1e9, 4), "unit": "Gkeys/s", "cores": thr,
+            "kind": kind,
+            "sample": (f"the first 4M x 8B keys bucketed by rank = CityHash64 % {nranks} into {form}: reference "
+                       f"CityHash64 per key, a count per rank and a stable scatter by rank (the Meraculous "
+                       f"count-then-ship shape, restated in oracle_time_bucket); {reps} bucketings per timing, "
+                       f"best of 5 ({best:.2f} s wall, {best * thr:.1f} CPU-s)"),
+            "timer": "CLOCK_MONOTONIC_RAW", "host": cpus, "gpu_digests_equal_reference": ok}
 
 
 if __name__ == "__main__":

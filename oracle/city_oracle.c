@@ -7,7 +7,9 @@
  * little-endian order, so the oracle does not depend on host endianness
  * (the reference's uint64_in_expected_order, city.c:50-75).
  */
-#define _POSIX_C_SOURCE 199309L
+#ifndef _POSIX_C_SOURCE
+#define _POSIX_C_SOURCE 200809L
+#endif
 #include "city_oracle.h"
 
 #include <pthread.h>
@@ -657,3 +659,115 @@ double oracle_time_batch(int mode, void *fn, const uint8_t *bytes, const uint64_
   clock_gettime(CLOCK_MONOTONIC_RAW, &t1);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---- CPU baseline of destination bucketing (bench.py bucket/records) ----- */
+/* The count-then-ship shape of the reference's bulk loader
+ * (bench/Meraculous/buildUFXhashBinary.h:103-109: hashfn per key,
+ * my_heap_sizes[rank]++, ufx_remote_thread[idx] = rank; the keys then go out
+ * grouped by rank, :255-279), as a parallel stable counting sort with
+ * `threads` pthreads over contiguous slices:
+ *   1. every thread hashes its slice (mbits = f64(key), rank = mbits %
+ *      nranks, real divides as hash.c:27/:29) and counts its ranks;
+ *   2. bucket offsets and per-(rank, thread) starts (thread 0's prefix);
+ *   3. every thread scatters its slice to the bucketed positions: arrays
+ *      (key, mbits, ptindex = mbits % nptes, original index), or with
+ *      `records` the wire record of bucket_records (type, src rank,
+ *      ht_index, index, mbits, key; stride 24 + keysize rounded up to 8).
+ * The same outputs as the GPU's pdht_bucket_batch_dev /
+ * pdht_bucket_records_dev.  Returns wall seconds of `reps` bucketings
+ * (CLOCK_MONOTONIC_RAW).  hist: threads * nranks uint32 of scratch. */
+typedef struct {
+  oracle_city64_fn f64;
+  const uint8_t *keys;
+  size_t L, lo, hi, n;
+  int t, threads, reps, records;
+  uint64_t nptes;
+  uint32_t nranks, src, ht;
+  uint64_t *mb;      /* [n] digests in key order */
+  uint32_t *rk;      /* [n] ranks in key order */
+  uint32_t *hist;    /* [threads][nranks]: counts, then start positions */
+  uint8_t *keys_out; /* arrays form */
+  uint64_t *mbits_out;
+  uint32_t *pt_out, *idx_out;
+  uint8_t *rec_out;  /* records form */
+  uint64_t *offsets; /* [nranks + 1] */
+  pthread_barrier_t *bar;
+} bkjob;
+
+static void *bucket_worker(void *arg) {
+  bkjob *j = (bkjob *)arg;
+  uint32_t *h = j->hist + (size_t)j->t * j->nranks;
+  const size_t rb = 24 + ((j->L + 7) & ~(size_t)7);
+  for (int r = 0; r < j->reps; ++r) {
+    memset(h, 0, (size_t)j->nranks * 4);
+    for (size_t i = j->lo; i < j->hi; ++i) {
+      const uint64_t m = j->f64((const char *)(j->keys + i * j->L), j->L);
+      const uint32_t k = (uint32_t)(m % j->nranks);
+      j->mb[i] = m;
+      j->rk[i] = k;
+      h[k]++;
+    }
+    pthread_barrier_wait(j->bar);
+    if (j->t == 0) { /* starts: rank-major, thread-minor (stable) */
+      uint64_t pos = 0;
+      for (uint32_t k = 0; k < j->nranks; ++k) {
+        j->offsets[k] = pos;
+        for (int t = 0; t < j->threads; ++t) {
+          uint32_t *c = j->hist + (size_t)t * j->nranks + k;
+          const uint32_t cnt = *c;
+          *c = (uint32_t)pos;
+          pos += cnt;
+        }
+      }
+      j->offsets[j->nranks] = pos;
+    }
+    pthread_barrier_wait(j->bar);
+    for (size_t i = j->lo; i < j->hi; ++i) {
+      const uint32_t p = h[j->rk[i]]++;
+      const uint64_t m = j->mb[i];
+      if (j->records) {
+        uint8_t *q = j->rec_out + (size_t)p * rb;
+        const uint32_t hdr[4] = {1u, j->src, j->ht, (uint32_t)i};
+        memcpy(q, hdr, 16);
+        memcpy(q + 16, &m, 8);
+        memcpy(q + 24, j->keys + i * j->L, j->L);
+        memset(q + 24 + j->L, 0, rb - 24 - j->L);
+      } else {
+        memcpy(j->keys_out + (size_t)p * j->L, j->keys + i * j->L, j->L);
+        j->mbits_out[p] = m;
+        j->pt_out[p] = (uint32_t)(m % j->nptes);
+        j->idx_out[p] = (uint32_t)i;
+      }
+    }
+    pthread_barrier_wait(j->bar);
+  }
+  return NULL;
+}
+
+double oracle_time_bucket(oracle_city64_fn fn, const uint8_t *keys, size_t L, size_t n, int threads,
+                          int reps, uint64_t nptes, uint32_t nranks, int records, uint32_t src,
+                          uint32_t ht, uint64_t *mb, uint32_t *rk, uint32_t *hist, uint8_t *keys_out,
+                          uint64_t *mbits_out, uint32_t *pt_out, uint32_t *idx_out, uint8_t *rec_out,
+                          uint64_t *offsets) {
+  if (threads < 1) threads = 1;
+  if (threads > 512) threads = 512;
+  pthread_t tid[512];
+  static bkjob jobs[512];
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)threads);
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC_RAW, &t0);
+  for (int t = 0; t < threads; ++t) {
+    bkjob j = {fn, keys, L, n * (size_t)t / (size_t)threads, n * (size_t)(t + 1) / (size_t)threads, n, t,
+               threads, reps, records, nptes ? nptes : 1, nranks ? nranks : 1, src, ht, mb, rk, hist,
+               keys_out, mbits_out, pt_out, idx_out, rec_out, offsets, &bar};
+    jobs[t] = j;
+    if (t > 0) pthread_create(&tid[t], NULL, bucket_worker, &jobs[t]);
+  }
+  bucket_worker(&jobs[0]);
+  for (int t = 1; t < threads; ++t) pthread_join(tid[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC_RAW, &t1);
+  pthread_barrier_destroy(&bar);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+

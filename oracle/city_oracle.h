@@ -104,6 +104,13 @@ double oracle_time_batch(int mode, void *fn, const uint8_t *bytes, const uint64_
                          size_t stride, size_t len, size_t n, int threads, int reps,
                          uint64_t nptes, uint64_t nranks, uint64_t *out, uint32_t *pt,
                          uint32_t *rk);
+/* CPU baseline of destination bucketing (bench.py bucket / records): hash,
+ * count per rank, stable scatter -- the same outputs as the GPU bucketing. */
+double oracle_time_bucket(oracle_city64_fn fn, const uint8_t *keys, size_t L, size_t n, int threads,
+                          int reps, uint64_t nptes, uint32_t nranks, int records, uint32_t src,
+                          uint32_t ht, uint64_t *mb, uint32_t *rk, uint32_t *hist, uint8_t *keys_out,
+                          uint64_t *mbits_out, uint32_t *pt_out, uint32_t *idx_out, uint8_t *rec_out,
+                          uint64_t *offsets);
 
 #ifdef __cplusplus
 }

@@ -91,6 +91,10 @@ def lib():
         L.oracle_time_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                         C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_uint64,
                                         C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_time_bucket.restype = C.c_double
+        L.oracle_time_bucket.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
+                                         C.c_uint64, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32]
+        L.oracle_time_bucket.argtypes += [C.c_void_p] * 9
         for name in ("oracle_apply64", "oracle_apply128"):
             f = getattr(L, name)
             f.restype = None
@@ -365,3 +369,43 @@ def time_batch(mode: int, fn: int, data: np.ndarray, n: int, *, offsets=None, L:
                                    nranks, _buf(out), _buf(pt) if pt is not None else None,
                                    _buf(rk) if rk is not None else None)
     return secs, out, pt, rk
+
+
+class BucketBufs:
+    """Output and scratch arrays of time_bucket (allocated once and touched,
+    so that first-touch page faults stay out of the timing)."""
+
+    def __init__(self, n: int, L: int, nranks: int, threads: int, records: bool):
+        self.mb = np.zeros(n, np.uint64)
+        self.rk = np.zeros(n, np.uint32)
+        self.hist = np.zeros(max(threads, 1) * nranks, np.uint32)
+        self.offsets = np.zeros(nranks + 1, np.uint64)
+        rb = 24 + (L + 7) // 8 * 8
+        if records:
+            self.rec = np.zeros((n, rb), np.uint8)
+            self.keys = self.mbits = self.pt = self.idx = None
+        else:
+            self.rec = None
+            self.keys = np.zeros((n, L), np.uint8)
+            self.mbits = np.zeros(n, np.uint64)
+            self.pt = np.zeros(n, np.uint32)
+            self.idx = np.zeros(n, np.uint32)
+
+
+def time_bucket(fn: int, keys: np.ndarray, nptes: int, nranks: int, *, threads: int = 1, reps: int = 1,
+                records: bool = False, src_rank: int = 0, ht_index: int = 0, bufs: BucketBufs | None = None):
+    """Wall seconds (CLOCK_MONOTONIC_RAW) of `reps` destination bucketings of
+    keys [n, L] with `threads` pthreads: hash (fn = CityHash64), count per
+    rank, stable scatter (oracle_time_bucket, the reference bulk loader's
+    count-then-ship shape).  Returns (secs, bufs): bufs holds the bucketed
+    arrays (keys, mbits, pt, idx) or records, and the offsets."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    n, L = keys.shape
+    b = bufs or BucketBufs(n, L, nranks, threads, records)
+    opt = lambda a: _buf(a) if a is not None else None  # noqa: E731
+    secs = lib().oracle_time_bucket(C.c_void_p(fn), _buf(keys), L, n, threads, reps, nptes, nranks,
+                                    int(records), src_rank, ht_index, _buf(b.mb), _buf(b.rk), _buf(b.hist),
+                                    opt(b.keys), opt(b.mbits), opt(b.pt), opt(b.idx), opt(b.rec),
+                                    _buf(b.offsets))
+    return secs, b
+

@@ -147,3 +147,24 @@ def test_oracle_matches_compiled_reference_fuzz(oracle):
         assert oracle.citycrc128(d) == (r.first, r.second)
         r = R.CityHash128(d, L)
         assert oracle.city128(d) == (r.first, r.second)
+
+
+def test_cpu_bucketing_baseline_is_the_stable_bucketing(oracle):
+    """bench.py's f4 CPU baseline (oracle_time_bucket: hash, count per rank,
+    stable scatter, the Meraculous count-then-ship shape) produces exactly the
+    reference placement stably bucketed -- the outputs the GPU bucketing is
+    checked against -- for 1 and several threads, arrays and records."""
+    k = oracle.fixed_keys(50_003, 8)
+    fn, _ = oracle.cpu_fn("CityHash64")
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, 1000)
+    order = np.argsort(r2, kind="stable")
+    want_offs = np.concatenate([[0], np.cumsum(np.bincount(r2, minlength=1000))])
+    for thr in (1, 3):
+        _, b = oracle.time_bucket(fn, k, 3, 1000, threads=thr, reps=2)
+        assert (b.offsets == want_offs).all() and (b.idx == order).all()
+        assert (b.mbits == m2[order]).all() and (b.pt == p2[order]).all() and (b.keys == k[order]).all()
+        _, b = oracle.time_bucket(fn, k, 3, 1000, threads=thr, records=True, src_rank=5, ht_index=3)
+        w32 = b.rec[:, :16].copy().view(np.uint32)
+        assert (w32[:, 0] == 1).all() and (w32[:, 1] == 5).all() and (w32[:, 2] == 3).all()
+        assert (w32[:, 3] == order).all() and (b.rec[:, 24:32] == k[order]).all()
+        assert (b.rec[:, 16:24].copy().view(np.uint64).ravel() == m2[order]).all()
