@@ -22,9 +22,8 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
            -Wall -Wno-unused-function -munsafe-fp-atomics -Iinclude
 CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
-HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/bucket.h \
-           pdht_amd/csrc/runtime.h pdht_amd/csrc/launch.h pdht_amd/csrc/pdht_hip_tuning.h \
-           include/pdht_hip.h include/pdht_city.h
+HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/runtime.h \
+           pdht_amd/csrc/pdht_hip_tuning.h include/pdht_hip.h include/pdht_city.h
 SHIM_HDR := include/pdht_hash.h include/pdht_hip.h include/pdht_city.h
 # the C-ABI in translation units that build in parallel (make -j)
 HIP_UNITS := pdht_hip pdht_fixed64 pdht_fixed128 pdht_var pdht_host pdht_bucket
@@ -38,6 +37,10 @@ OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
 all: product oracle
 
 product: $(LIB) $(LIB_MPI) $(LIB_TUN)
+
+# unit-specific headers
+$(LIBDIR)/pdht_bucket.o $(LIBDIR)/pdht_bucket.tun.o: pdht_amd/csrc/bucket.h
+$(foreach u,pdht_fixed64 pdht_fixed128 pdht_var pdht_host,$(LIBDIR)/$(u).o $(LIBDIR)/$(u).tun.o): pdht_amd/csrc/launch.h
 
 $(LIBDIR)/%.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 	@mkdir -p $(LIBDIR)

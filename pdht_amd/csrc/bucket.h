@@ -420,6 +420,7 @@ __device__ __forceinline__ void copy_row(uint8_t *dst, const uint8_t *src, u32 L
 // OutSoA (pdht_bucket_batch_dev): separate arrays, each but mbits optional.
 struct OutSoA {
   static constexpr bool kPair8 = false;
+  static constexpr bool kJoint = false;
   uint8_t *keys;
   u64 *mbits;
   u32 *ptindex;
@@ -451,8 +452,14 @@ struct OutSoA {
 //   struct's alignment padding)  +16 u64 mbits  +24 key[L], zero-padded to
 //   the record stride 24 + round_up(L, 8).
 // One record per key means one run per bucket and tile instead of four.
-struct OutRec {
+// JOINT (8-B keys): both 16-B halves of a record leave back to back, once the
+// key has been staged, instead of the header half first and the {mbits, key}
+// half a staging round later (by then the header halves' lines had often left
+// L2 half-written: 2.1x the record bytes reached HBM, r02 PMC).
+template <bool JOINT>
+struct OutRecT {
   static constexpr bool kPair8 = true;  // 8-B keys: 32-B records written as two 16-B halves
+  static constexpr bool kJoint = JOINT;
   uint8_t *rec;
   u64 stride;
   u64 hdr;  // type | rank << 32
@@ -486,6 +493,7 @@ struct OutRec {
     for (u32 j = L; j < stride - 24; ++j) d[j] = 0;
   }
 };
+typedef OutRecT<true> OutRec;
 
 // Phase D/E of the staged scatters: thread j writes staged entry j (digest in
 // stage[j]) to slot delta[digit(h)] + j with original index idx(j); then the
@@ -497,6 +505,33 @@ __device__ __forceinline__ void staged_store(u64 *stage, const u32 *delta, u32 t
                                              const Out &out) {
   constexpr int kPer = KPL;  // entries per thread: a tile is kB x KPL keys
   u32 gp[kPer];
+  if constexpr (Out::kPair8 && L == 8 && Out::kJoint) {
+    // 8-B keys into 32-B records, both 16-B halves ({header, index} and
+    // {mbits, key}) stored together once the keys are staged
+    u64 hv[kPer];
+    u32 si[kPer];
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 j = min(jj * kB + threadIdx.x, tn - 1);
+      hv[jj] = stage[j];
+      gp[jj] = delta[dig(hv[jj], j)] + j;
+      si[jj] = j;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < KPL; ++g)
+      if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < kPer; ++jj) {
+      const u32 j = jj * kB + threadIdx.x;
+      if (j < tn) {
+        out.head(gp[jj], idx(si[jj]));
+        out.tail8(gp[jj], hv[jj], stage[j]);
+      }
+    }
+    return;
+  }
   if constexpr (Out::kPair8 && L == 8) {
     // 8-B keys into 32-B records: two 16-B stores per record, {header,
     // index} and {mbits, key}, half the store instructions of four 8-B ones

@@ -321,6 +321,15 @@ struct AlgoLenOnly {
     return len;
   }
 };
+// Timing only: CityHash64 twice per key (the second over the key minus its
+// first byte), to see what the hash arithmetic itself costs a kernel.
+struct AlgoCity64x2 {
+  typedef u64 Out;
+  template <class R>
+  __device__ __forceinline__ Out operator()(const R &r, u64 len) const {
+    return city64(r, len) ^ (len ? city64(Shifted<R>{r, 1u}, len - 1) : 0);
+  }
+};
 #endif
 
 // ----------------------------------------------------------------- sinks ---

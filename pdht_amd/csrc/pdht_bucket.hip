@@ -475,5 +475,11 @@ PDHT_API int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n,
   if ((uintptr_t)records & 7) return fail("records must be 8-byte aligned%s", "");
   const OutRec out{static_cast<uint8_t *>(records), (u64)pdht_bucket_record_bytes(keysize),
                    (u64)msg_type | ((u64)src_rank << 32), ht_index, (u32)keysize};
+#ifdef PDHT_HIP_TUNING
+  if (tuning_variant() == 112) {  // r02 store order: header halves first, {mbits, key} halves a round later
+    const OutRecT<false> o2{out.rec, out.stride, out.hdr, out.ht_index, out.L};
+    return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, o2, 0, bucket_offsets, ST(s));
+  }
+#endif
   return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, out, 0, bucket_offsets, ST(s));
 }

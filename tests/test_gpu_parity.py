@@ -579,6 +579,8 @@ RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 54, 58) for L in (8, 16, 32) fo
 RECORD_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (7, 1000, 8192)
                  for n in (4097, 300007)]
 RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n in (4097, (2 << 20) + 9)]
+# 112: the r02 store order of 8-B records (header halves a staging round early)
+RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
 # records switch to owner-table ranking for 16/32-B keys from 512 ranks while
 # two workgroups fit a CU (staged_shape): both edges of both thresholds
 RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]

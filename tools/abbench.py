@@ -35,7 +35,9 @@ def workload(name, dev):
         kind, L, nr = name.split("_")
         L, nr, n = int(L), int(nr), 16 * M
         keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
-        ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
+        with P.tuning(0):  # the tuning build reserves the two-pass intermediate at any nranks
+            wsb = P.bucket_workspace_bytes(n, L, nr)
+        ws = torch.empty(max(wsb, P.bucket_workspace_bytes(n, L, nr)), dtype=torch.uint8, device=dev)
         if kind == "records":
             outs = P.bucket_records(keys, nr, workspace=ws)
             return ((lambda: P.bucket_records(keys, nr, out=outs, workspace=ws)),
@@ -81,7 +83,9 @@ def workload(name, dev):
             outs = P.place_batch(keys, 3, 1024)
             return ((lambda: P.place_batch(keys, 3, 1024, hist=hist, out=outs)),
                     (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 24)
-        ws = torch.empty(P.bucket_workspace_bytes(n, 8, 1024), dtype=torch.uint8, device=dev)
+        with P.tuning(0):
+            wsb = P.bucket_workspace_bytes(n, 8, 1024)
+        ws = torch.empty(max(wsb, P.bucket_workspace_bytes(n, 8, 1024)), dtype=torch.uint8, device=dev)
         outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
         return ((lambda: P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)),
                 (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (8 + 8 + 8 + 4 + 4))
