@@ -69,8 +69,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5", "place", "bucket", "bucket8k", "exchange", "records",
-                             "xrecords", "long"])
+                    choices=["cfg1", "cfg2", "cfg2r", "cfg3", "cfg4", "cfg5", "place", "bucket", "bucket8k", "exchange",
+                             "records", "xrecords", "long"])
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true")
@@ -254,13 +254,27 @@ def main():
         bytes_per_key = 64 + 8 + 4 + 4
         workload = f"cfg1: pdht_hash placement (mbits+ptindex+rank+hist) of {n >> 20}M x 64B keys per GPU"
         total_bytes_in = n * L
-    elif cfg in ("cfg2", "cfg4", "cfg5", "place"):
+    elif cfg in ("cfg2", "cfg2r", "cfg4", "cfg5", "place"):
         L = 8 if cfg == "place" else 64
         n = a.keys_per_gpu or (128 * M if cfg == "cfg5" else 16 * M)
         sh = D.weak_shard(rank, world, n)
         words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
-        if cfg in ("cfg2", "cfg5"):
+        if cfg == "cfg2r":
+            # cfg2 with the digests written round-robin into 4 buffers (4 x 128
+            # MiB): between two writes of one buffer 4 GiB of keys and 384 MiB
+            # of other digests pass, so no digest line can wait in the 256 MiB
+            # Infinity Cache for its next overwrite -- every step's digests
+            # reach HBM, as cfg5's 1 GiB of digests must
+            import itertools
+            rot = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(4)]
+            turn = itertools.cycle(range(4))
+            out = rot[0]
+            step = lambda: P.city64_batch(keys, out=rot[next(turn)])  # noqa: E731
+            bytes_per_key = 64 + 8
+            workload = (f"cfg2r: CityHash64 over {n >> 20}M x 64B keys per GPU, device-resident, digests written "
+                        f"round-robin into 4 buffers (every step's digests reach HBM)")
+        elif cfg in ("cfg2", "cfg5"):
             out = torch.empty(n, dtype=torch.int64, device=dev)
             step = lambda: P.city64_batch(keys, out=out)  # noqa: E731
             bytes_per_key = 64 + 8
@@ -348,7 +362,7 @@ def main():
         calib = round(keys.numel() / (cms / 1e3) / 1e9, 1)
     # the 64-B kernel's own data movement with the hash replaced by an XOR fold
     calib_key = None
-    if cfg in ("cfg2", "cfg5"):
+    if cfg in ("cfg2", "cfg2r", "cfg5"):
         fold = torch.empty(n, dtype=torch.int64, device=dev)
         P.key_stream(keys, out=fold)
         cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -385,13 +399,18 @@ def main():
         if cfg in ("place", "cfg1"):  # one fresh call: the timed ones accumulated into hist
             hist.zero_()
             extra = (*P.place_batch(keys, *((1, 4) if cfg == "cfg1" else (3, 1024)), hist=hist), hist)
-        parity = check_parity(P, torch, D, cfg, sh, out, extra, dev)
+        if cfg == "cfg2r":
+            ps = [check_parity(P, torch, D, "cfg2", sh, r, None, dev) for r in rot]
+            parity = ps[0] if all(p.startswith("ok") for p in ps) else "FAILED: " + " | ".join(ps)
+            parity += f" (all {len(rot)} rotating digest buffers)"
+        else:
+            parity = check_parity(P, torch, D, cfg, sh, out, extra, dev)
 
     # ------------------------------------------------------- report ------
     value = n * world * a.steps / elapsed_max / 1e9
     achieved = bytes_per_key * n / (kern_ms / 1e3) / 1e9
     res = {
-        "metric": METRIC if cfg in ("cfg2", "cfg5") else f"{cfg}: Gkeys/s and achieved HBM GB/s",
+        "metric": METRIC if cfg in ("cfg2", "cfg5", "cfg2r") else f"{cfg}: Gkeys/s and achieved HBM GB/s",
         "value": round(value, 4),
         "unit": "Gkeys/s",
         "n_gpus": world,
@@ -420,7 +439,7 @@ def main():
     if world > 1:
         res["per_rank"] = D.per_rank_report(rank, local, world, n, bytes_per_key, kern_ms, elapsed, a.steps,
                                             PEAK_HBM_GBPS, device=dev)
-    if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:
+    if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:  # (cfg2r: the same host path as cfg2)
         hr = host_rate(P, torch, n, cfg, D, dev)
         if rank == 0:
             res["host_resident"] = hr
@@ -710,7 +729,7 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
         s_n, mode, nptes, nranks = M, 2, 1, 4
         data = O.fixed_keys(s_n, 64)
         what = "all 1M x 64B keys of cfg1, per-key pdht_hash semantics (nptes 1, nranks 4)"
-    elif cfg in ("cfg2", "cfg5"):
+    elif cfg in ("cfg2", "cfg2r", "cfg5"):
         s_n = 4 * M
         data = O.fixed_keys(s_n, 64)
         what = "the first 4M x 64B keys of the stream"
@@ -760,13 +779,13 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
     ok = None
     if gpu_out is not None:
         g = gpu_out.reshape(-1)[: dig.size].cpu().numpy().view(np.uint64)
-        if cfg == "cfg3" or cfg in ("cfg1", "cfg2", "cfg4", "cfg5", "long", "place"):
+        if cfg == "cfg3" or cfg in ("cfg1", "cfg2", "cfg2r", "cfg4", "cfg5", "long", "place"):
             ok = bool((dig[: g.size] == g).all()) if g.size == dig.size else None
     res = {"value": round(s_n * reps / best / 1e9, 4), "unit": "Gkeys/s", "cores": thr, "kind": kind,
            "sample": f"{what}; {reps} passes per timing, best of 5 ({best:.2f} s wall, "
                      f"{best * thr:.1f} CPU-s)",
            "timer": "CLOCK_MONOTONIC_RAW", "host": cpus, "gpu_digests_equal_reference": ok}
-    if cfg in ("cfg2", "cfg5"):
+    if cfg in ("cfg2", "cfg2r", "cfg5"):
         # BASELINE.md §3's other leg on the same box: one thread through
         # per-key pdht_hash over cfg1's 1M x 64 B keys
         k1 = O.fixed_keys(M, 64)

@@ -352,6 +352,7 @@ struct Sink64T {
   __device__ __forceinline__ void init() {}
   __device__ __forceinline__ void put(u64 i, u64 h) { st<NTS>(h, out + i); }
   __device__ __forceinline__ void flush() {}
+  __host__ Sink64T shift(u64 k0) const { return Sink64T{lds_hist, out + k0}; }  // keys from k0 on
 };
 template <bool NTS = false>
 struct Sink128T {
@@ -365,6 +366,7 @@ struct Sink128T {
     st<NTS>(v, reinterpret_cast<u64x2 *>(out) + i);
   }
   __device__ __forceinline__ void flush() {}
+  __host__ Sink128T shift(u64 k0) const { return Sink128T{lds_hist, out + 2 * k0}; }
 };
 typedef Sink64T<false> Sink64;
 typedef Sink128T<false> Sink128;
@@ -443,6 +445,13 @@ struct SinkPlaceT {
       for (u32 r = threadIdx.x; r < nranks; r += blockDim.x)
         if (lds_hist[r]) atomicAdd(reinterpret_cast<unsigned long long *>(hist + r), (unsigned long long)lds_hist[r]);
     }
+  }
+  __host__ SinkPlaceT shift(u64 k0) const {
+    SinkPlaceT s = *this;
+    s.mbits += k0;
+    if (s.ptindex) s.ptindex += k0;
+    if (s.rank) s.rank += k0 * s.rank_stride;
+    return s;
   }
 };
 typedef SinkPlaceT<false> SinkPlace;

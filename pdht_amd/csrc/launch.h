@@ -68,8 +68,52 @@ static bool sink_has_hist(const Sink &s) {
 // Fixed-length keys: the register-direct / LDS-transposed kernels for the
 // specialised lengths when the layout allows them, else the window kernel
 // (a 64-key tile fits 12 or 16 KiB of LDS), else per-lane global reads.
+// Batches larger than this many key bytes go out as consecutive launches of
+// about this size.  One persistent launch over a multi-GiB batch streams
+// ~10 % slower than the same keys in 1 GiB launches (tools/abbench.py:
+// cfg5 = 128M x 64 B in one launch 1.814 ms; as 8 launches of 16M keys
+// 8 x 0.206 ms): over a long launch the waves drift apart, and the memory
+// the chip has in flight spreads over ever more of the buffer.
+constexpr u64 kLaunchBytes = 1ull << 30;
+static u64 launch_chunk_bytes() {
+#ifdef PDHT_HIP_TUNING
+  switch (tuning_variant()) {  // 114-118: chunk 256 MiB / 512 MiB / 2 GiB / 4 GiB / one launch
+    case 114: return 256ull << 20;
+    case 115: return 512ull << 20;
+    case 116: return 2ull << 30;
+    case 117: return 4ull << 30;
+    case 118: return ~0ull;
+    default: break;
+  }
+#endif
+  return kLaunchBytes;
+}
+
 template <class Algo, class Sink>
-static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo,
+static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
+                            hipStream_t st);
+
+// Fixed-length keys in launches of about launch_chunk_bytes() each.
+template <class Algo, class Sink>
+static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
+                        hipStream_t st) {
+  const u64 per = std::max<u64>(1, launch_chunk_bytes() / std::max<u64>(stride, 1));
+  if (n <= per || stride == 0) return launch_fixed_one(keys, stride, keylen, n, algo, sink, st);
+  const u64 step = (per + 4095) & ~(u64)4095;  // whole 64-key tiles (and 4096-key blocks)
+  const char *tag = "";
+  for (u64 k0 = 0; k0 < n; k0 += step) {
+    const u64 c = std::min<u64>(step, n - k0);
+    if (int rc = launch_fixed_one(static_cast<const uint8_t *>(keys) + k0 * stride, stride, keylen, c, algo,
+                                  sink.shift(k0), st))
+      return rc;
+    if (k0 == 0) tag = g_kernel;
+  }
+  g_kernel = tag;  // the tag of the full-size launches
+  return 0;
+}
+
+template <class Algo, class Sink>
+static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo,
                         Sink sink, hipStream_t st) {
   if (n == 0) return 0;
   if (!keys && keylen) return fail("null key pointer%s", "");  // empty keys read nothing
@@ -257,7 +301,31 @@ static void launch_sorted(const uint8_t *b, const u64 *offsets, u64 obase, size_
 // 1-3 KiB keys: the window's DMA pulls the lines into L2 for the keys that
 // overflow it.)
 template <class Algo, class Sink>
+static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
+                          Sink sink, hipStream_t st);
+
+// Variable-length keys in launches of about launch_chunk_bytes() of key bytes
+// each (split by key count at the batch's mean length; every launch keeps the
+// whole batch's window choice).
+template <class Algo, class Sink>
 static int launch_var(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
+                      Sink sink, hipStream_t st) {
+  const u64 lim = launch_chunk_bytes();
+  if (n == 0 || nbytes <= lim) return launch_var_one(bytes, nbytes, offsets, obase, n, algo, sink, st);
+  const u64 mean = std::max<u64>(1, nbytes / n);
+  const u64 step = std::max<u64>(4096, (lim / mean) & ~(u64)4095);
+  const char *tag = "";
+  for (u64 k0 = 0; k0 < n; k0 += step) {
+    const u64 c = std::min<u64>(step, n - k0);
+    if (int rc = launch_var_one(bytes, mean * c, offsets + k0, obase, c, algo, sink.shift(k0), st)) return rc;
+    if (k0 == 0) tag = g_kernel;
+  }
+  g_kernel = tag;
+  return 0;
+}
+
+template <class Algo, class Sink>
+static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
                       Sink sink, hipStream_t st) {
   if (n == 0) return 0;
   if (!bytes || !offsets) return fail("null bytes/offsets pointer%s", "");

@@ -884,3 +884,42 @@ def test_batches_capture_in_hip_graph(dev, oracle):
         assert (u64(pl[0]) == m2).all() and (pl[2].cpu().numpy().view(np.uint32) == r2).all()
         order = np.argsort(r2, kind="stable")
         assert (bk[3].cpu().numpy().view(np.uint32) == order).all() and (u64(bk[1]) == m2[order]).all()
+
+
+@pytest.mark.parametrize("variant", [0, 114])
+def test_chunked_launches(dev, oracle, variant):
+    """Batches past launch_chunk_bytes() go out as consecutive launches (1 GiB
+    in the product, 256 MiB in tuning variant 114): fixed keys (digests,
+    128-bit digests, fused placement with a histogram and ptl_process_t-style
+    rank stride) and offset-indexed keys, ragged ends, checked against the
+    oracle on samples from both sides of every chunk boundary."""
+    n = (5 << 20) + 4099  # 320 MiB of 64-B keys: two 256 MiB launches in variant 114
+    words = P.splitmix64_fill(0x77, 0, n * 8, device=dev)
+    kd = words.view(torch.uint8).view(n, 64)
+    step = (256 << 20) // 64
+    idx = np.unique(np.concatenate([np.arange(0, 200), np.arange(step - 100, step + 100),
+                                    np.arange(n - 200, n)]))
+    kh = kd[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    with P.tuning(variant) if variant else _nullctx():
+        d64 = u64(P.city64_batch(kd))
+        d128 = u64(P.city128_batch(kd)).reshape(-1, 2)
+        hist = torch.zeros(1000, dtype=torch.int64, device=dev)
+        mb, pt, rk = P.place_batch(kd, 3, 1000, hist=hist)
+    assert (d64[idx] == oracle.city64_fixed(kh)).all()
+    assert (d128[idx] == oracle.city128_fixed(kh)).all()
+    m2, p2, r2 = oracle.pdht_hash_fixed(kh, 3, 1000)
+    assert (u64(mb)[idx] == m2).all() and (pt.cpu().numpy().view(np.uint32)[idx] == p2).all()
+    r_all = rk.cpu().numpy().view(np.uint32)
+    assert (r_all[idx] == r2).all() and (u64(mb) % 1000 == r_all).all()
+    assert (hist.cpu().numpy() == np.bincount(r_all, minlength=1000)).all()
+    # variable-length keys: 3M mixed 16..256 B = ~408 MB
+    nv = 3 << 20
+    lens = P.mixed_lengths(0x1E575EED1E575EED, 0, nv, 16, 256, device=dev)
+    offs = torch.zeros(nv + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item())
+    data = P.splitmix64_fill(0x5EED5EED5EED5EED, 0, (total + 7) // 8, device=dev).view(torch.uint8)[:total]
+    with P.tuning(variant) if variant else _nullctx():
+        dv = u64(P.city64_var_batch(data, offs))
+    dh, oh = data.cpu().numpy(), offs.cpu().numpy().astype(np.uint64)
+    assert (dv == oracle.city64_var(dh, oh)).all()

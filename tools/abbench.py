@@ -60,6 +60,21 @@ def workload(name, dev):
         outs = P.place_batch(keys, 1, 4, hist=hist)
         return ((lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)),
                 (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 80)
+    if name in ("cfg5rot", "cfg5fix", "cfg5roto"):
+        # 16M-key slices of cfg5's 128M-key buffer: rotating / always slice 3
+        # (one 128 MiB digest buffer); roto: rotating keys AND digest slices
+        # of a 1 GiB digest buffer
+        n, L = 16 * M, 64
+        keys = P.splitmix64_fill(SEED, 0, 8 * n * L // 8, device=dev).view(torch.uint8).view(8 * n, L)
+        out = torch.empty(8 * n if name == "cfg5roto" else n, dtype=torch.int64, device=dev)
+        turn = [0]
+
+        def step():
+            j = turn[0] % 8 if name != "cfg5fix" else 3
+            turn[0] += 1
+            o = out[j * n:(j + 1) * n] if name == "cfg5roto" else out
+            P.city64_batch(keys[j * n:(j + 1) * n], out=o)
+        return step, (lambda: out[:1].clone()), n * (L + 8)
     if name in ("long128", "long128s"):  # 2M x 512 B CityHash128 (city.c:378-400) / WithSeed (:310-376)
         n, L = 2 * M, 512
         keys = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L)
