@@ -1009,361 +1009,6 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict
   }
 }
 
-// ------------------------------------------------------ gather scatter ---
-// The store pattern sets the rate: a stable counting sort writes, per input
-// tile and bucket, one run into every output array, and the write path runs
-// at ~1.2 TB/s for 16-B runs, ~2.1 for 32-B, ~3.6 for 64-B and ~4.5 for
-// >= 128-B runs (tools/scatter_probe.hip, r02).  A 4096-key tile over 1024
-// buckets gives 4-key runs (32 B of an 8-B array, 16 B of a 4-B one); the
-// staged kernel's time is that store time.  This kernel sorts a tile of
-// W x KPL x 64 keys (default 8 x 32 x 64 = 16384: 16-key runs, 128 B / 64 B)
-// and stages ONLY the sorted order in LDS (u16 per key): the store phase
-// gathers each key back from L2 (the count phase just read it with the
-// default cache policy) and hashes it again, so the LDS per key is 2 B
-// instead of 10 and two such workgroups fit a CU (68 KiB at 1024 buckets),
-// one storing while the other sorts.
-//   A: hash the wave's keys (rr[g] = bucket), count them into run[w][r];
-//   B: tile-local bucket starts (block scan); delta[r] = global start of the
-//      tile's run of bucket r - its tile-local start;
-//   C: each key's tile-local sorted slot lp (ballot rank within its group of
-//      64, group leader claims the run with one LDS atomic); sidx[lp] = key;
-//   D: thread j takes sorted slots j, j+W*64, ...: key gathered (batches of
-//      CH, all loads issued before any store so one wait covers them), hash,
-//      bucket, global slot delta[r] + slot, stores.
-// LK = key length when it is 8/16/32 (keys in registers), 0 = any length
-// (GlobalReader / byte copies).
-constexpr int kGaW = 8, kGaKPL = 32;
-constexpr size_t gather_lds_bytes(u32 nranks, int W, int KPL) {
-  return (size_t)W * nranks * 4 + (size_t)nranks * 4 + (size_t)W * KPL * 64 * 2;
-}
-// DBG (tuning build only, timing-only, wrong results): bit 0 = no global
-// stores in D, bit 1 = no gather in D (the slot's own index stands in),
-// bit 2 = no phase D at all.
-// CH = slots per thread gathered before any is stored: every gather's wait
-// is a vmcnt wait, which on CDNA also waits for every store issued before it,
-// so each batch boundary costs a store round trip (8-B keys: the whole
-// tile's 32 slots in one batch).
-template <int LK, class Out, int W = kGaW, int KPL = kGaKPL,
-          int CH = ((LK == 32 ? 8 : LK == 16 ? 16 : 32) < KPL ? (LK == 32 ? 8 : LK == 16 ? 16 : 32) : KPL),
-          int DBG = 0>
-__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W == 8 ? 4 : 8)))
-void k_bucket_scatter_gather(const uint8_t *__restrict__ keys, u32 L, u64 n,
-                                                                  FastMod rk, u32 nranks, u32 nbits,
-                                                                  TileStarts ts, u64 ntiles, Out out) {
-  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
-  static_assert(kTile <= 65536, "u16 tile offsets");
-  static_assert(KPL % CH == 0, "store batches");
-  extern __shared__ u32 lds32[];
-  const RunTab<false> run{lds32, nranks};
-  u32 *delta = lds32 + W * nranks;                                // [nranks]
-  uint16_t *sidx = reinterpret_cast<uint16_t *>(delta + nranks);  // [kTile]
-  __shared__ u32 scan_scratch[W];
-  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const u32 per = (nranks + kB - 1) / kB;
-  const u32 rb0 = min(threadIdx.x * per, nranks), rb1 = min(rb0 + per, nranks);
-  auto hash_at = [&](u64 i) -> u64 {
-    if constexpr (LK != 0) {
-      RegReader<LK / 4> kr;
-      load_key_regs<LK, false>(keys, i, kr);
-      return city64(kr, (u64)LK);
-    } else {
-      return city64(GlobalReader{keys + i * (u64)L}, (u64)L);
-    }
-  };
-  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
-    const u64 t = o.t;
-    const u64 tbase = t * kTile;
-    const u32 tn = (u32)min((u64)kTile, n - tbase);
-    for (u32 j = threadIdx.x; j < W * nranks; j += kB) run.t[j] = 0;
-    const u32 q0 = wave * kSub + lane;
-    u32 rr[KPL];
-    if constexpr (LK != 0) {
-      constexpr int kA = LK == 8 ? 8 : 4;  // keys in flight per lane
-#pragma unroll
-      for (int g0 = 0; g0 < KPL; g0 += kA) {
-        RegReader<LK / 4> kr[kA];
-#pragma unroll
-        for (int g = 0; g < kA; ++g)
-          load_key_regs<LK, false>(keys, min(tbase + q0 + (g0 + g) * 64, n - 1), kr[g]);
-#pragma unroll
-        for (int g = 0; g < kA; ++g) rr[g0 + g] = (u32)rk.mod(city64(kr[g], (u64)LK));
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) rr[g] = (u32)rk.mod(hash_at(min(tbase + q0 + g * 64, n - 1)));
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) run.add(wave, rr[g], 1u);
-    __syncthreads();
-    u32 s = 0;
-    for (u32 r = rb0; r < rb1; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) s += run.get(w, r);
-    u32 acc = block_exclusive_scan<W>(s, scan_scratch);
-    for (u32 r = rb0; r < rb1; ++r) {
-      delta[r] = ts.at(r, t) - acc;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const u32 v = run.get(w, r);
-        run.set(w, r, acc);
-        acc += v;
-      }
-    }
-    __syncthreads();
-    rank_and_place<KPL, 8>(run, wave, rr, q0, tn, nbits, sidx);
-    __syncthreads();
-#pragma unroll 1
-    for (int c0 = 0; c0 < ((DBG & 4) ? 0 : KPL); c0 += CH) {
-      u32 idx[CH];
-#pragma unroll
-      for (int c = 0; c < CH; ++c) idx[c] = sidx[min((c0 + c) * kB + threadIdx.x, tn - 1)];
-      if constexpr (LK != 0) {
-        RegReader<LK / 4> kr[CH];
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          if constexpr (DBG & 2) {
-            kr[c].d[0] = idx[c];
-            for (int q = 1; q < LK / 4; ++q) kr[c].d[q] = q;
-          } else {
-            load_key_regs<LK, false>(keys, tbase + idx[c], kr[c]);
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const u32 j = (c0 + c) * kB + threadIdx.x;
-          if (DBG & 1) {
-            if (city64(kr[c], (u64)LK) == 0x123456789ull) out.meta(0, 0, 0);  // never
-            continue;
-          }
-          if (j < tn) {
-            const u64 h = city64(kr[c], (u64)LK);
-            const u64 gp = delta[(u32)rk.mod(h)] + j;
-            if constexpr (Out::kPair8 && LK == 8) {
-              out.head(gp, tbase + idx[c]);
-              out.tail8(gp, h, (u64)kr[c].d[0] | ((u64)kr[c].d[1] << 32));
-            } else {
-              out.meta(gp, h, tbase + idx[c]);
-              if (out.has_keys()) out.template key_row<LK>(gp, kr[c]);
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const u32 j = (c0 + c) * kB + threadIdx.x;
-          if (j < tn) {
-            const u64 i = tbase + idx[c];
-            const u64 h = hash_at(i);
-            const u64 gp = delta[(u32)rk.mod(h)] + j;
-            out.meta(gp, h, i);
-            if (out.has_keys()) out.key_copy(gp, keys + i * (u64)L);
-          }
-        }
-      }
-    }
-    __syncthreads();  // run, delta and sidx are rewritten by the next tile
-  }
-}
-
-// ---------------------------------------------- producer/consumer scatter ---
-// k_bucket_scatter_gather with its phases overlapped inside ONE workgroup:
-// waves 0..WP-1 (producers) sort tile s+1 -- hash, count, scan, rank, sorted
-// order into sidx[buffer] -- while waves WP..2WP-1 (consumers) store tile s
-// from the other buffer.  Two workgroups of the gather kernel start their
-// tiles together and store together; here the stores are spread over the
-// producers' whole tile.  Both roles pass the same __syncthreads sequence
-// (4 per step).  Consumers store their slots over the step's four
-// intervals, each interval's keys gathered one interval ahead.  8-B keys.
-template <class Out, int WP = 8, int KPL = 32>
-__global__ __launch_bounds__(2 * WP * 64) __attribute__((amdgpu_waves_per_eu(4)))
-void k_bucket_scatter_pc(const uint8_t *__restrict__ keys, u32 L, u64 n, FastMod rk, u32 nranks, u32 nbits,
-                         TileStarts ts, u64 ntiles, Out out) {
-  constexpr u32 kTile = WP * KPL * 64, kP = WP * 64, kSub = KPL * 64;
-  static_assert(kTile <= 65536, "u16 tile offsets");
-  static_assert(KPL % 4 == 0, "four store intervals");
-  constexpr int kQ = KPL / 4;  // consumer slots stored per interval
-  extern __shared__ u32 lds32[];
-  const RunTab<false> run{lds32, nranks};                           // producers' [WP][nranks]
-  u32 *const delta_b = lds32 + WP * nranks;                         // [2][nranks]
-  uint16_t *const sidx_b = reinterpret_cast<uint16_t *>(delta_b + 2 * nranks);  // [2][kTile]
-  __shared__ u32 scan_scratch[2 * WP];
-  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool producer = wave < WP;  // wave-uniform
-  const u32 per = (nranks + kP - 1) / kP;
-  const u32 rb0 = producer ? min(threadIdx.x * per, nranks) : nranks;
-  const u32 rb1 = producer ? min(rb0 + per, nranks) : nranks;
-  const u32 q0 = wave * kSub + lane;  // producers' first key of the tile
-  const u32 cj = threadIdx.x - kP;    // consumers' first slot
-  TileOrder o(ntiles);
-  u64 tp = o.t;       // producer's tile this step
-  u64 tc = ~0ull;     // consumer's tile this step (none in the first step)
-  int b = 0;          // buffer the producers fill this step
-  while (tp < o.end || tc != ~0ull) {  // the same for every thread
-    const bool have_p = tp < o.end, have_c = tc != ~0ull;
-    const u64 pbase = tp * kTile, cbase = tc * kTile;
-    const u32 ptn = have_p ? (u32)min((u64)kTile, n - pbase) : 0;
-    const u32 ctn = have_c ? (u32)min((u64)kTile, n - cbase) : 0;
-    u32 rr2[KPL / 2];  // producers: bucket ids, two u16 per register
-    const uint16_t *csidx = sidx_b + (b ^ 1) * kTile;
-    const u32 *cdelta = delta_b + (b ^ 1) * nranks;
-    // consumers: the keys of interval q's slots are gathered during interval
-    // q-1 and the stores of interval q follow interval q+1's gather, so the
-    // compiler's wait for a gather is vmcnt(#stores issued since), not a
-    // drain; stores are unconditional (slots past a partial tile's end
-    // repeat its last slot: the same bytes to the same place)
-    RegReader<2> kc[2][kQ];
-    u32 ci[2][kQ];
-    auto gather = [&](int q, int sl) {
-#pragma unroll
-      for (int c = 0; c < kQ; ++c) {
-        ci[sl][c] = csidx[min((q * kQ + c) * kP + cj, ctn - 1)];
-        load_key_regs<8, false>(keys, cbase + ci[sl][c], kc[sl][c]);
-      }
-    };
-    // ---- interval 1: zero runs, load + hash (P) | gather (C)
-    if (producer) {
-      for (u32 j = threadIdx.x; j < WP * nranks; j += kP) run.t[j] = 0;
-      if (have_p) {
-#pragma unroll
-        for (int g0 = 0; g0 < KPL; g0 += 8) {
-          RegReader<2> kr[8];
-#pragma unroll
-          for (int g = 0; g < 8; ++g) load_key_regs<8, false>(keys, min(pbase + q0 + (g0 + g) * 64, n - 1), kr[g]);
-#pragma unroll
-          for (int g = 0; g < 8; g += 2)
-            rr2[(g0 + g) / 2] = (u32)rk.mod(city64(kr[g], 8)) | ((u32)rk.mod(city64(kr[g + 1], 8)) << 16);
-        }
-      }
-    } else if (have_c) {
-      gather(0, 0);
-    }
-    auto store_q = [&](int q) {  // consumers: gather q+1, then store interval q
-      if (!producer && have_c) {
-        const int sl = q & 1;
-        if (q + 1 < 4) gather(q + 1, sl ^ 1);
-#pragma unroll
-        for (int c = 0; c < kQ; ++c) {
-          const u32 j = min((q * kQ + c) * kP + cj, ctn - 1);
-          const u64 h = city64(kc[sl][c], 8);
-          const u64 gp = cdelta[(u32)rk.mod(h)] + j;
-          if constexpr (Out::kPair8) {
-            out.head(gp, cbase + ci[sl][c]);
-            out.tail8(gp, h, (u64)kc[sl][c].d[0] | ((u64)kc[sl][c].d[1] << 32));
-          } else {
-            out.meta(gp, h, cbase + ci[sl][c]);
-            if (out.has_keys()) out.template key_row<8>(gp, kc[sl][c]);
-          }
-        }
-      }
-    };
-    store_q(0);
-    __syncthreads();
-    // ---- interval 2: count (P) | stores (C)
-    if (producer && have_p) {
-#pragma unroll
-      for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < ptn) run.add(wave, (rr2[g / 2] >> (16 * (g & 1))) & 0xffffu, 1u);
-    }
-    store_q(1);
-    __syncthreads();
-    // ---- interval 3: scan (P; every thread takes part, consumers with 0) | stores (C)
-    u32 sum = 0;
-    for (u32 r = rb0; r < rb1; ++r)
-#pragma unroll
-      for (int w = 0; w < WP; ++w) sum += run.get(w, r);
-    u32 acc = block_exclusive_scan<2 * WP>(sum, scan_scratch);
-    if (producer && have_p) {
-      u32 *pdelta = delta_b + b * nranks;
-      for (u32 r = rb0; r < rb1; ++r) {
-        pdelta[r] = ts.at(r, tp) - acc;
-#pragma unroll
-        for (int w = 0; w < WP; ++w) {
-          const u32 v = run.get(w, r);
-          run.set(w, r, acc);
-          acc += v;
-        }
-      }
-    }
-    store_q(2);
-    __syncthreads();
-    // ---- interval 4: rank + place (P) | stores (C)
-    if (producer && have_p) {
-      u32 rr[KPL];
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) rr[g] = (rr2[g / 2] >> (16 * (g & 1))) & 0xffffu;
-      rank_and_place<KPL, 8>(run, wave, rr, q0, ptn, nbits, sidx_b + b * kTile);
-    }
-    store_q(3);
-    __syncthreads();
-    tc = have_p ? tp : ~0ull;
-    tp = have_p ? tp + o.step : tp;
-    b ^= 1;
-  }
-}
-
-// ------------------------------------------- register scatter (no staging) ---
-// Tile = W waves x KPL groups; keys, digests and ranks stay in VGPRs, so the
-// scatter pass issues no loads: on CDNA a load wait is a vmcnt wait, which
-// also counts the scattered stores already in flight.
-template <int W, int L, int KPL, class Out>
-__global__ __launch_bounds__(W * 64) void k_bucket_scatter_reg(const uint8_t *__restrict__ keys, u64 n,
-                                                               FastMod rk, u32 nranks, u32 nbits,
-                                                               TileStarts ts, u64 ntiles, Out out) {
-  extern __shared__ u32 run[];  // [W][nranks]
-  constexpr u64 kSub = (u64)KPL * 64, kTile = W * kSub;
-  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const u64 below = (1ull << lane) - 1;
-  u32 *myrun = run + wave * nranks;
-  for (TileOrder o(ntiles); o.t < o.end; o.t += o.step) {
-    const u64 t = o.t;
-    for (u32 j = threadIdx.x; j < W * nranks; j += W * 64) run[j] = 0;
-    const u64 k0 = t * kTile + wave * kSub + lane;
-    RegReader<L / 4> kr[KPL];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(k0 + (u64)g * 64, n - 1), kr[g]);
-    u64 h[KPL];
-    u32 rr[KPL];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) {
-      h[g] = city64(kr[g], (u64)L);
-      rr[g] = (u32)rk.mod(h[g]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (k0 + (u64)g * 64 < n) atomicAdd(&myrun[rr[g]], 1u);
-    __syncthreads();
-    for (u32 r = threadIdx.x; r < nranks; r += W * 64) {
-      u32 acc = ts.at(r, t);
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const u32 v = run[w * nranks + r];
-        run[w * nranks + r] = acc;
-        acc += v;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) {
-      const u64 i = k0 + (u64)g * 64;
-      const bool valid = i < n;
-      const u64 same = same_bucket_lanes(valid, rr[g], nbits);
-      const u32 ahead = (u32)__builtin_popcountll(same & below);
-      const u32 pos = valid ? myrun[rr[g]] + ahead : 0;
-      wave_lds_sync();
-      if (valid && ahead == 0) myrun[rr[g]] += (u32)__builtin_popcountll(same);
-      if (valid) {
-        out.meta(pos, h[g], i);
-        if (out.has_keys()) out.template key_row<L>(pos, kr[g]);
-      }
-      wave_lds_sync();
-    }
-    __syncthreads();
-  }
-}
-
 // ------------------------------------------------- generic-length scatter ---
 // Tile = W waves x 32 groups; wave w owns a contiguous 2048-key sub-range.
 // Counting pass hashes; the scatter pass hashes again from L2-resident keys

@@ -341,25 +341,6 @@ PDHT_HD u128 murmur128(const R &s, u64 len, u128 seed) {
   return u128{a ^ b, mix16(b, a)};
 }
 
-// Tuning A/B only: CityHash128's 16-B shifted loop on line spans (measured
-// no faster than the plain 64-B spans, r02).
-template <class R, class = void>
-struct ReaderLines16 {
-  static constexpr bool value = false;
-};
-template <class R>
-struct ReaderLines16<R, decltype((void)R::kLines16)> {
-  static constexpr bool value = R::kLines16;
-};
-template <class R, class = void>
-struct ReaderOneCarry {
-  static constexpr bool value = false;
-};
-template <class R>
-struct ReaderOneCarry<R, decltype((void)R::kOneCarry)> {
-  static constexpr bool value = R::kOneCarry;
-};
-
 // city.c:369-375
 PDHT_HD u128 city128_final(u64 x, u64 y, u64 z, u128 v, u128 w) {
   x = mix16(x, v.lo);
@@ -395,74 +376,39 @@ PDHT_HD u128 city128_finish(const R &s, u32 o, u64 rem, const LongState &st) {
   return city128_final(x, y, z, v, w);
 }
 
-// city.c:310-376 for len >= 128 on kPairs readers, the hashed bytes starting
-// SH (0 or 16: CityHash128's seed bytes) into a key whose 128-B lines the
-// reader fetches whole.  Each 128-byte iteration is one line load: with SH =
-// 16 the iteration's bytes are the rest of line j (112 B, carried in
-// registers from the previous load) and the head of line j+1; the last
-// iteration loads only the 16 B it needs when line j+1 would pass the key.
-template <int SH, class R>
+// city.c:310-376 for len >= 128 on kPairs readers (keys whose 128-B lines
+// the reader fetches whole): each 128-byte iteration is one line load.
+// (CityHash128 hashes from byte 16 on, so its iterations straddle lines; a
+// form that loaded whole lines and carried the 112-B remainder in registers
+// measured 5 % slower than plain 64-B spans, r02, and was removed.)
+template <class R>
 PDHT_HD u128 city128_seed_lines(const R &b, u64 len, u128 seed) {
-  static_assert(SH == 0 || SH == 16, "seed bytes: none or 16");
-  const u64 total = len + SH;
   LongState st;
   st.x = seed.lo;
   st.y = seed.hi;
   st.z = len * kK1;
-  Words<32> l0 = b.template span<128>(0);  // total >= 128 + SH
-  st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + l0.w64(SH);
-  st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + l0.w64(SH + 8);
+  Words<32> l0 = b.template span<128>(0);  // len >= 128
+  st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + l0.w64(0);
+  st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + l0.w64(8);
   st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
-  st.w.hi = rotr_nz(st.x + l0.w64(SH + 88), 53) * kK1;
+  st.w.hi = rotr_nz(st.x + l0.w64(88), 53) * kK1;
   u32 o = 0;
   u64 rem = len;
-  if constexpr (SH == 0) {
-    do {
-      if (o) l0 = b.template span<128>(o);
-      round64(st, sub_words<32, 0, 16>(l0));
-      round64(st, sub_words<32, 16, 16>(l0));
-      o += 128;
-      rem -= 128;
-    } while (rem >= 128);
-  } else {
-    // two carry arrays used in turn (a single one cost 28 register moves
-    // per iteration on the loop's back edge)
-    Words<28> ca = sub_words<32, 4, 28>(l0), cb;
-    auto iter = [&](const Words<28> &cin, Words<28> &cout) -> bool {
-      Words<32> q;
-#pragma unroll
-      for (int i = 0; i < 28; ++i) q.d[i] = cin.d[i];
-      if ((u64)o + 256 <= total) {  // uniform for fixed-length batches
-        const Words<32> ld = b.template span<128>(o + 128);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q.d[28 + i] = ld.d[i];
-        cout = sub_words<32, 4, 28>(ld);
-      } else {  // last iteration (the next would need o + 144 + 128 <= total)
-        const Words<4> t = b.template span<16>(o + 128);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q.d[28 + i] = t.d[i];
-      }
-      round64(st, sub_words<32, 0, 16>(q));
-      round64(st, sub_words<32, 16, 16>(q));
-      o += 128;
-      rem -= 128;
-      return rem >= 128;
-    };
-    if constexpr (ReaderOneCarry<R>::value) {  // tuning A/B: one carry array
-      while (iter(ca, cb)) ca = cb;
-    } else {
-      while (iter(ca, cb) && iter(cb, ca)) {
-      }
-    }
-  }
-  return city128_finish(Shifted<R>{b, (u32)SH}, o, rem, st);
+  do {
+    if (o) l0 = b.template span<128>(o);
+    round64(st, sub_words<32, 0, 16>(l0));
+    round64(st, sub_words<32, 16, 16>(l0));
+    o += 128;
+    rem -= 128;
+  } while (rem >= 128);
+  return city128_finish(b, o, rem, st);
 }
 
 // city.c:310-376
 template <class R>
 PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
   if (len < 128) return murmur128(s, len, seed);
-  if constexpr (ReaderPairs<R>::value) return city128_seed_lines<0>(s, len, seed);
+  if constexpr (ReaderPairs<R>::value) return city128_seed_lines(s, len, seed);
   LongState st;
   st.x = seed.lo;
   st.y = seed.hi;
@@ -490,8 +436,6 @@ template <class R>
 PDHT_HD u128 city128(const R &s, u64 len) {
   if (len >= 16) {
     const Words<4> h = s.template span<16>(0);
-    if constexpr (ReaderLines16<R>::value)
-      if (len >= 144) return city128_seed_lines<16>(s, len - 16, u128{h.w64(0) ^ kK3, h.w64(8)});
     return city128_seed(Shifted<R>{s, 16}, len - 16, u128{h.w64(0) ^ kK3, h.w64(8)});
   }
   if (len >= 8) {
@@ -530,33 +474,13 @@ PDHT_HD u32 crc32c_slice8(const Crc32cTables &T, u64 x) {
          T.t[3][(x >> 32) & 0xff] ^ T.t[2][(x >> 40) & 0xff] ^ T.t[1][(x >> 48) & 0xff] ^ T.t[0][x >> 56];
 }
 
-// The same map in 5-bit slices: CRC-32C of a 64-bit word with a zero initial
+// The same map in 6-bit slices: CRC-32C of a 64-bit word with a zero initial
 // CRC is GF(2)-linear in the word, so it is the XOR of the contributions of
-// its 13 five-bit fields (12 x 5 bits + the top 4), each a 32-entry table:
-// T5[k][f] = crc(f << 5k).  13 lookups instead of 8, but a 32-entry table
-// spans 32 distinct LDS banks, so 64 lanes reading one table at random
-// indices never conflict (identical indices broadcast); slicing-by-8's
-// 256-entry tables conflicted 4.3x (profiles/r01/sq_long).
-struct Crc32c5Tables {
-  u32 t[13][32];
-};
-constexpr Crc32c5Tables make_crc32c5_tables() {
-  Crc32c5Tables F{};
-  const Crc32cTables S = make_crc32c_tables();
-  for (u32 k = 0; k < 13; ++k)
-    for (u32 f = 0; f < 32; ++f) {
-      const u64 x = k < 12 || f < 16 ? (u64)f << (5 * k) : 0;
-      F.t[k][f] = S.t[7][x & 0xff] ^ S.t[6][(x >> 8) & 0xff] ^ S.t[5][(x >> 16) & 0xff] ^
-                  S.t[4][(x >> 24) & 0xff] ^ S.t[3][(x >> 32) & 0xff] ^ S.t[2][(x >> 40) & 0xff] ^
-                  S.t[1][(x >> 48) & 0xff] ^ S.t[0][x >> 56];
-    }
-  return F;
-}
-__device__ __constant__ const Crc32c5Tables kCrc5Dev = make_crc32c5_tables();
-
-// 6-bit slices: 11 fields (10 x 6 bits + the top 4), 64-entry tables.  A
-// 64-word table spans each of the 64 LDS banks once, so random indices are
-// still conflict-free, and a word costs 11 lookups instead of 13.
+// its 11 six-bit fields (10 x 6 bits + the top 4), each a 64-entry table:
+// T6[k][f] = crc(f << 6k).  11 lookups instead of 8, but 64 lanes reading one
+// 64-word table at random indices never conflict in LDS (identical indices
+// broadcast; slicing-by-8's 256-entry tables conflicted 4.3x,
+// profiles/r01/sq_long); r02's 5-bit form took 13 lookups per word.
 struct Crc32c6Tables {
   u32 t[11][64];
 };
@@ -575,7 +499,7 @@ constexpr Crc32c6Tables make_crc32c6_tables() {
 __device__ __constant__ const Crc32c6Tables kCrc6Dev = make_crc32c6_tables();
 
 // Where the tables live: CrcConstTab = the compile-time slicing-by-8 tables
-// (host; device constant memory); kernels.h adds the LDS copy of the 5-bit
+// (host; device constant memory); kernels.h adds the LDS copy of the 6-bit
 // tables for the GPU's long-key path.
 struct CrcConstTab {
   PDHT_HD u32 crc64(u64 x) const {

@@ -201,46 +201,10 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
       constexpr int kPerCu = kShort ? 2 : 8;
       if (al16 && stride % 16 == 0) {
 #ifdef PDHT_HIP_TUNING
-        if (tuning_variant() == 93) {  // CRC-256 blocks as whole lines
-          g_kernel = "k_global<fixed,a16,lines>";
-          k_global<false, Algo, SinkNt, true, 3><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
-        if (tuning_variant() == 98) {  // + CityHash128's shifted loop on line spans
-          g_kernel = "k_global<fixed,a16,lines16>";
-          k_global<false, Algo, SinkNt, true, 7><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
-        if (tuning_variant() == 95 || tuning_variant() == 97) {  // 128-B spans (97: one carry array)
-          g_kernel = tuning_variant() == 95 ? "k_global<fixed,a16,pairs>" : "k_global<fixed,a16,lines16,1carry>";
-          if (tuning_variant() == 97)
-            k_global<false, Algo, SinkNt, true, 6><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          else
-            k_global<false, Algo, SinkNt, true, 4><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
         if (tuning_variant() == 96) {  // r02 before the line spans: 240-B / 64-B spans as the algorithm reads them
           g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
           k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
               k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
-        if (tuning_variant() == 91 || tuning_variant() == 92) {  // nt span loads (all / all but the last line)
-          g_kernel = tuning_variant() == 91 ? "k_global<fixed,a16,nt>" : "k_global<fixed,a16,nt-head>";
-          if (tuning_variant() == 91)
-            k_global<false, Algo, SinkNt, true, 1><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          else
-            k_global<false, Algo, SinkNt, true, 2><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-                k, nullptr, 0, stride, keylen, n, algo, sink_nt);
           HIP_TRY(hipGetLastError());
           return 0;
         }
@@ -267,39 +231,6 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
   return 0;
 }
 
-// Length-sorted window kernel (k_window_sorted): W waves per workgroup,
-// PER_CU workgroups per CU; the window takes what the CU's 160 KiB leave
-// after the sort tables (10 B per key), the histogram and the CRC tables.
-template <class Algo>
-constexpr int crc_lds_bytes() {
-  if constexpr (HasCrcLds<Algo>::value)
-    return (int)(Algo::Slices::kWords * 4);
-  else
-    return 0;
-}
-template <int W, int PER_CU, class Algo, class Sink>
-constexpr int sorted_winb() {
-  constexpr int crc = crc_lds_bytes<Algo>();
-  constexpr int fixed = 64 * W * 10 + W * (int)kSortBins * 4 + 16 + 4 * (int)Sink::kHist + crc + 64;
-  return (163840 / PER_CU - fixed) / 16 * 16;
-}
-template <int W, int PER_CU, class Algo, class Sink>
-static void launch_sorted(const uint8_t *b, const u64 *offsets, u64 obase, size_t n, Algo algo, Sink sink,
-                          hipStream_t st, int dev, const char *tag) {
-  constexpr int WINB = sorted_winb<W, PER_CU, Algo, Sink>();
-  g_kernel = tag;
-  const u64 tiles = (n + 64 * W - 1) / (64 * W);
-  k_window_sorted<W, WINB, Algo, Sink, 2><<<grid_for(tiles, PER_CU, dev), 64 * W, 0, st>>>(b, offsets, obase, n,
-                                                                                         algo, sink);
-}
-
-// Variable-length keys.  `nbytes` = key bytes the batch spans
-// (offsets[n] - offsets[0]; 0 = unknown) sizes the LDS window for the mean
-// key length (tools/varbench.py, r01): mean <= 160 B (cfg3's 16..256 mix,
-// mean 136) -> 10224 B per wave at 4 workgroups/CU; longer -> 16 KiB at 2.
-// (Per-lane global reads measured slower than the 16 KiB window even at
-// 1-3 KiB keys: the window's DMA pulls the lines into L2 for the keys that
-// overflow it.)
 template <class Algo, class Sink>
 static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
                           Sink sink, hipStream_t st);
@@ -324,6 +255,15 @@ static int launch_var(const void *bytes, u64 nbytes, const u64 *offsets, u64 oba
   return 0;
 }
 
+// One launch over variable-length keys.  `nbytes` = key bytes the batch
+// spans (offsets[n] - offsets[0]; 0 = unknown) sizes the LDS window for the
+// mean key length (r01): mean <= 160 B (cfg3's 16..256 mix, mean 136) ->
+// 10224 B per wave at 4 workgroups/CU; longer -> 16 KiB at 2.  (Per-lane
+// global reads measured slower than the 16 KiB window even at 1-3 KiB keys:
+// the window's DMA pulls the lines into L2 for the keys that overflow it.
+// r02/r03 measured a double-buffered window, offsets prefetched a tile
+// ahead, the next window prefetched in VGPRs, 128-B window alignment and
+// length-sorted workgroup windows: none faster)
 template <class Algo, class Sink>
 static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64 obase, size_t n, Algo algo,
                       Sink sink, hipStream_t st) {
@@ -339,81 +279,6 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
 #ifdef PDHT_HIP_TUNING
   if (tuning_variant() == 12) wide = false;
   if (tuning_variant() == 13) wide = true;
-  // 100-105: the length-sorted window kernel, W waves per workgroup @ per CU
-  // (nt = non-temporal digest stores, else plain)
-  switch (tuning_variant()) {
-    case 100: launch_sorted<8, 2>(b, offsets, obase, n, algo, sink_nt, st, dev, "k_window_sorted<8,nt>@2"); break;
-    case 101: launch_sorted<8, 2>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<8>@2"); break;
-    case 102: launch_sorted<4, 3>(b, offsets, obase, n, algo, sink_nt, st, dev, "k_window_sorted<4,nt>@3"); break;
-    case 103: launch_sorted<4, 3>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<4>@3"); break;
-    case 104: launch_sorted<4, 4>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<4>@4"); break;
-    case 105: launch_sorted<16, 1>(b, offsets, obase, n, algo, sink, st, dev, "k_window_sorted<16>@1"); break;
-    default: break;
-  }
-  if constexpr (BufStore<Sink>::kOk) {
-    if (tuning_variant() == 106 || tuning_variant() == 107) {  // next window in VGPRs (106: nt stores)
-      g_kernel = tuning_variant() == 106 ? "k_window_pf<10K,nt>@4" : "k_window_pf<10K>@4";
-      if (tuning_variant() == 106)
-        k_window_pf<10240, Algo, SinkNt><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                  sink_nt);
-      else
-        k_window_pf<10240, Algo, Sink><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo, sink);
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-  }
-  if (tuning_variant() >= 100 && tuning_variant() <= 105) {
-    HIP_TRY(hipGetLastError());
-    return 0;
-  }
-  if (tuning_variant() == 46) {  // windows start on a 128-B line
-    g_kernel = "k_window<var,nt,10224,a128>@4";
-    k_window<10224, true, Algo, SinkNt, 2, 128><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0,
-                                                                                       n, algo, sink_nt);
-    HIP_TRY(hipGetLastError());
-    return 0;
-  }
-  if (tuning_variant() >= 23 && tuning_variant() <= 25) {  // double-buffered windows
-    if (tuning_variant() == 23) {
-      g_kernel = "k_window_db<10224>@2";
-      k_window_db<10224, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                 sink_nt);
-    } else if (tuning_variant() == 24) {
-      g_kernel = "k_window_db<6656>@3";
-      k_window_db<6656, Algo, SinkNt, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                sink_nt);
-    } else {
-      g_kernel = "k_window_db<8192>@2";
-      k_window_db<8192, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                sink_nt);
-    }
-    HIP_TRY(hipGetLastError());
-    return 0;
-  }
-  if (tuning_variant() == 48 || tuning_variant() == 49) {  // next window prefetched in VGPRs (48: nt loads)
-    g_kernel = tuning_variant() == 48 ? "k_window_rp<10224,nt>@4" : "k_window_rp<10224>@4";
-    if (tuning_variant() == 48)
-      k_window_rp<10224, Algo, SinkNt, true><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                    sink_nt);
-    else
-      k_window_rp<10224, Algo, SinkNt, false><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                     sink_nt);
-    HIP_TRY(hipGetLastError());
-    return 0;
-  }
-  if (tuning_variant() == 30 || tuning_variant() == 31) {  // offsets prefetched one tile ahead
-    if (tuning_variant() == 31 || wide) {
-      g_kernel = "k_window_var<16K>@2";
-      k_window_var<16384, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                  sink_nt);
-    } else {
-      g_kernel = "k_window_var<10224>@4";
-      k_window_var<10224, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                  sink_nt);
-    }
-    HIP_TRY(hipGetLastError());
-    return 0;
-  }
 #endif
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";

@@ -117,20 +117,7 @@ static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, in
   return 0;
 }
 
-#ifdef PDHT_HIP_TUNING
-template <int W, int L, int KPL, class Out>
-static int launch_reg(const BucketArgs &a, const Out &out, hipStream_t st, int dev) {
-  static const char *const names[3] = {"k_bucket_scatter_reg<8B>", "k_bucket_scatter_reg<16B>",
-                                       "k_bucket_scatter_reg<32B>"};
-  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
-  const size_t bytes = (size_t)W * a.nranks * 4;
-  if (int rc = set_lds(reinterpret_cast<const void *>(&k_bucket_scatter_reg<W, L, KPL, Out>), bytes)) return rc;
-  k_bucket_scatter_reg<W, L, KPL, Out><<<grid_for(a.ntiles, 2, dev), W * 64, bytes, st>>>(
-      a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
-  return 0;
-}
 
-#endif
 
 template <int W, class Out>
 static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st, int dev) {
@@ -142,25 +129,7 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
   return 0;
 }
 
-#ifdef PDHT_HIP_TUNING
-template <int W, int KPL, class Out>
-static int launch_gather(const BucketArgs &a, const Out &out, u32 L, int lk, hipStream_t st, int dev) {
-  const size_t bytes = gather_lds_bytes(a.nranks, W, KPL);
-  const int per_cu = bytes <= 80 * 1024 ? 2 : 1;
-  auto go = [&](auto fn, const char *name) -> int {
-    g_kernel = name;
-    if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
-    unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
-    if (g >= 8) g &= ~7u;  // a multiple of 8: XCD-contiguous tile order (TileOrder)
-    fn<<<g, W * 64, bytes, st>>>(a.k, L, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
-    return 0;
-  };
-  if (lk == 8) return go(&k_bucket_scatter_gather<8, Out, W, KPL>, "k_bucket_scatter_gather<8B>");
-  if (lk == 16) return go(&k_bucket_scatter_gather<16, Out, W, KPL>, "k_bucket_scatter_gather<16B>");
-  if (lk == 32) return go(&k_bucket_scatter_gather<32, Out, W, KPL>, "k_bucket_scatter_gather<32B>");
-  return go(&k_bucket_scatter_gather<0, Out, W, KPL>, "k_bucket_scatter_gather<any>");
-}
-#endif
+
 
 
 template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false>
@@ -198,26 +167,14 @@ static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &ou
 template <int L, class Out>
 static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
                                u32 *tickets) {
-#ifdef PDHT_HIP_TUNING
-  // 73-76: sub-tile shape (waves x keys per lane) and workgroups per CU;
-  // 77: 73 with contiguous stores (timing-only, wrong results); 86: per-XCD
-  // tile tickets
-  switch (tuning_variant()) {
-    case 73: return launch_two_pass<L, Out, 4, 8, 4>(a, tp, out, st, dev, tickets);
-    case 74: return launch_two_pass<L, Out, 8, 4, 4>(a, tp, out, st, dev, tickets);
-    case 75: return launch_two_pass<L, Out, 4, 16, 2>(a, tp, out, st, dev, tickets);
-    case 76: return launch_two_pass<L, Out, 4, 4, 6>(a, tp, out, st, dev, tickets);
-    case 77: return launch_two_pass<L, Out, 4, 8, 4, 1>(a, tp, out, st, dev, tickets);  // timing-only
-    case 86: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, true>(a, tp, out, st, dev, tickets);
-    default: break;
-  }
-#endif
+  // (r02 A/B of sub-tile shapes, 8 x 4 / 4 x 16 / 4 x 4 keys and 2-6 WG/CU,
+  // and of per-XCD tile tickets: the product shape was best or equal)
   return launch_two_pass<L, Out>(a, tp, out, st, dev, tickets);
 }
 
-enum class BucketKernel { kGather, kStaged, kReg, kGeneric, kTwoPass };
+enum class BucketKernel { kStaged, kGeneric, kTwoPass };
 
-enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16, kOwner4x24 };
+enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16 };
 template <class Out>
 static StagedShape staged_shape(size_t keysize, u32 nranks) {
   if (nranks < 512) return StagedShape::kBallot4x16;
@@ -251,8 +208,8 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   if (!workspace || workspace_bytes < w.bytes) return fail("workspace too small%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
-  // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter up to
-  // 2048 ranks, register scatter above; other lengths -> generic.
+  // Kernel choice: packed 8/16/32-B keys (aligned) -> LDS-staged scatter below
+  // the two-pass threshold, two passes from it; other lengths -> generic.
   const uintptr_t al = (uintptr_t)keys | out_al;
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
   // (two_pass_min_ranks <= kStagedMaxRanks + 1: the staged scatter covers
@@ -260,23 +217,16 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   BucketKernel kind = !fixed                                ? BucketKernel::kGeneric
                       : nranks >= two_pass_min_ranks(keysize) ? BucketKernel::kTwoPass
                                                               : BucketKernel::kStaged;
-  int ga_w = kGaW, ga_kpl = kGaKPL;
 #ifdef PDHT_HIP_TUNING
-  // 21 generic, 22 register scatter; 54 the gather scatter (16384-key tiles,
-  // keys gathered back from L2 and re-hashed), 52 / 53 it with 8192-key
-  // tiles (4 waves x 32 / 8 waves x 16 keys per lane); 55-57 its timing-only
-  // builds; 58 producer/consumer scatter; 50 staged with u16 run tables.
-  // All measured slower than the staged scatter.
-  // 70: one pass (staged / register scatter) at any nranks; 71: two passes
-  // at any nranks >= 2.
-  if (tuning_variant() == 70 && kind == BucketKernel::kTwoPass)
-    kind = nranks > kStagedMaxRanks ? BucketKernel::kReg : BucketKernel::kStaged;
+  // 21: the generic-length kernel for 8/16/32-B keys too; 70: one pass (the
+  // staged scatter) up to 2048 ranks whatever the two-pass threshold; 71:
+  // two passes at any nranks >= 2.  (r02's gather, producer/consumer and
+  // register scatters measured slower than the staged one and were removed
+  // in r03: DESIGN.md §4.4.)
+  if (tuning_variant() == 70 && kind == BucketKernel::kTwoPass && nranks <= kStagedMaxRanks)
+    kind = BucketKernel::kStaged;
   if (tuning_variant() == 71 && fixed && nranks >= 2) kind = BucketKernel::kTwoPass;
   if (tuning_variant() == 21) kind = BucketKernel::kGeneric;
-  if (tuning_variant() == 22 && fixed) kind = BucketKernel::kReg;
-  if (tuning_variant() >= 52 && tuning_variant() <= 58 && nranks <= kStagedMaxRanks) kind = BucketKernel::kGather;
-  if (tuning_variant() == 52) ga_w = 4;
-  if (tuning_variant() == 53) ga_kpl = 16;
 #endif
   // Staged scatter shape (tools/abbench.py): owner-table
   // ranking for array outputs from 512 ranks; with it, 8 waves x 16 keys per
@@ -286,18 +236,16 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   // CU (<= 1462 ranks); ballots below 512 ranks and for records.
   StagedShape shape = staged_shape<Out>(keysize, nranks);
 #ifdef PDHT_HIP_TUNING
+  // 83 / 87: owner ranking on 8 x 16 / 4 x 16 tiles, 85 / 89: ballots, at any
+  // nranks (85 also in the static tile order)
   if (tuning_variant() == 83) shape = StagedShape::kOwner8x16;
   if (tuning_variant() == 87) shape = StagedShape::kOwner4x16;
-  if (tuning_variant() == 84 && keysize == 8) shape = StagedShape::kOwner4x24;
   if (tuning_variant() == 85 || tuning_variant() == 89) shape = StagedShape::kBallot4x16;
 #endif
-  const u64 st_tile = shape == StagedShape::kOwner8x16 ? 8192 : shape == StagedShape::kOwner4x24 ? 6144 : kStTile;
-  const int waves = nranks <= 4096 ? 8 : 4;  // reg / generic: W x nranks x 4 B of LDS <= 128 KiB
-  const int reg_kpl = keysize == 32 ? 8 : 16;
-  const u64 tile = kind == BucketKernel::kGather     ? (u64)ga_w * ga_kpl * 64
-                   : kind == BucketKernel::kTwoPass ? kTpCountTile
-                   : kind == BucketKernel::kStaged   ? st_tile
-                   : kind == BucketKernel::kReg    ? (u64)waves * reg_kpl * 64
+  const u64 st_tile = shape == StagedShape::kOwner8x16 ? 8192 : kStTile;
+  const int waves = nranks <= 4096 ? 8 : 4;  // generic: W x nranks x 4 B of LDS <= 128 KiB
+  const u64 tile = kind == BucketKernel::kTwoPass ? kTpCountTile
+                   : kind == BucketKernel::kStaged ? st_tile
                                                    : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
@@ -371,43 +319,10 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   if (ntiles) {
     int rc = 0;
 #ifdef PDHT_HIP_TUNING
-    const int lk = fixed ? (int)keysize : 0;
-    if (kind == BucketKernel::kGather && !(tuning_variant() >= 55 && tuning_variant() <= 58 && lk == 8)) {
-      if (ga_w == 8 && ga_kpl == 32)
-        rc = launch_gather<8, 32>(a, out, (u32)keysize, lk, st, dev);
-      else if (ga_w == 4)
-        rc = launch_gather<4, 32>(a, out, (u32)keysize, lk, st, dev);
-      else
-        rc = launch_gather<8, 16>(a, out, (u32)keysize, lk, st, dev);
-    } else if (kind == BucketKernel::kGather && lk == 8 && tuning_variant() == 58) {
-      // producer/consumer scatter: 8 + 8 waves, 16384-key tiles, 1 WG/CU
-      const size_t bytes = (size_t)8 * a.nranks * 4 + (size_t)2 * a.nranks * 4 + (size_t)2 * 16384 * 2;
-      auto fn = &k_bucket_scatter_pc<Out, 8, 32>;
-      g_kernel = "k_bucket_scatter_pc<8B>";
-      if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
-      unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus));
-      if (g >= 8) g &= ~7u;
-      fn<<<g, 1024, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
-    } else if (kind == BucketKernel::kGather && ga_w == 8 && ga_kpl == 32 && lk == 8 &&
-               tuning_variant() >= 55 && tuning_variant() <= 57) {
-      // timing-only builds (wrong results): 55 no stores, 56 no gather, 57 no phase D
-      const size_t bytes = gather_lds_bytes(a.nranks, 8, 32);
-      const int v = tuning_variant();
-      auto fn = v == 55 ? &k_bucket_scatter_gather<8, Out, 8, 32, 32, 1>
-                : v == 56 ? &k_bucket_scatter_gather<8, Out, 8, 32, 32, 2>
-                          : &k_bucket_scatter_gather<8, Out, 8, 32, 32, 4>;
-      g_kernel = "k_bucket_scatter_gather<8B,timing-only>";
-      if (int e = set_lds(reinterpret_cast<const void *>(fn), bytes)) return e;
-      unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * 2) & ~7u;
-      fn<<<g, 512, bytes, st>>>(a.k, (u32)keysize, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out);
-    } else if (kind == BucketKernel::kStaged && tuning_variant() == 85)  // static tile order (r02 default before)
+    if (kind == BucketKernel::kStaged && tuning_variant() == 85)  // static tile order (r02 default before)
       rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
            : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
                            : launch_staged<32, Out>(a, out, st, dev);
-    else if (kind == BucketKernel::kStaged && tuning_variant() == 50)  // u16 run tables, 3 WG/CU
-      rc = keysize == 8    ? launch_staged<8, Out, true>(a, out, st, dev)
-           : keysize == 16 ? launch_staged<16, Out, true>(a, out, st, dev)
-                           : launch_staged<32, Out, true>(a, out, st, dev);
     else
 #endif
     if (kind == BucketKernel::kTwoPass)
@@ -422,21 +337,10 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
       rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets)
                            : launch_staged<32, Out, false, kStW, kStKPL, true, 2>(a, out, st, dev, w.tickets);
-#ifdef PDHT_HIP_TUNING
-    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner4x24)  // slower (spills)
-      rc = launch_staged<8, Out, false, 4, 24, true, 2>(a, out, st, dev, w.tickets);
-#endif
     else if (kind == BucketKernel::kStaged)  // per-XCD tile tickets
       rc = keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets)
                            : launch_staged<32, Out, false, kStW, kStKPL, true>(a, out, st, dev, w.tickets);
-#ifdef PDHT_HIP_TUNING
-    else if (kind == BucketKernel::kReg)
-      rc = keysize == 8 ? (waves == 8 ? launch_reg<8, 8, 16>(a, out, st, dev) : launch_reg<4, 8, 16>(a, out, st, dev))
-           : keysize == 16
-               ? (waves == 8 ? launch_reg<8, 16, 16>(a, out, st, dev) : launch_reg<4, 16, 16>(a, out, st, dev))
-               : (waves == 8 ? launch_reg<8, 32, 8>(a, out, st, dev) : launch_reg<4, 32, 8>(a, out, st, dev));
-#endif
     else
       rc = waves == 8 ? launch_wg<8>(a, out, (u32)keysize, st, dev) : launch_wg<4>(a, out, (u32)keysize, st, dev);
     if (rc) return rc;

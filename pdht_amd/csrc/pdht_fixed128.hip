@@ -21,10 +21,6 @@ PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t k
                                        uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
   if (keylen > 900) {  // CityHashCrc256 rounds: CRC-32C tables in LDS
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 90)  // 5-bit slices, 13 lookups per word (r02 before the 6-bit tables)
-      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 5>{}, Sink128{nullptr, out}, ST(s));
-#endif
     return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
   }
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));

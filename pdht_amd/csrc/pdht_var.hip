@@ -32,31 +32,23 @@ PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const
 #ifdef PDHT_HIP_TUNING
   // data-movement calibrations of the window kernel (no LDS reads, digest =
   // key length): 40 as shipped; 41 default-policy DMA; 42 plain stores;
-  // 43 as 40 at 3 WG/CU; 44 offsets prefetched (k_window_var)
+  // 43 as 40 at 3 WG/CU; 45 windows on 128-B lines
   const int v = tuning_variant();
-  if (v >= 108 && v <= 111) {
-    // 108 / 109: the register-prefetched window (k_window_pf) with a
-    // length-only / fold digest; 110 / 111: the product window kernel with
-    // CityHash64 twice per key / once (what the arithmetic costs)
+  if (v == 110 || v == 111) {
+    // the product window kernel with CityHash64 twice per key (110) / once
+    // (111): what the hash arithmetic costs over the data movement (40)
     if (n == 0) return 0;
     int dev;
     if (int rc = current_device(&dev)) return rc;
     const uint8_t *b = static_cast<const uint8_t *>(bytes);
     const u64 wb = ((n + 63) / 64 + 3) / 4;
     const Sink64T<true> snt{nullptr, out};
-    hipStream_t st = ST(s);
     g_kernel = "k_window<var,calib>";
-    if (v == 108)
-      k_window_pf<10240, AlgoLenOnly, Sink64T<true>><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, 0, n,
-                                                                                            AlgoLenOnly{}, snt);
-    else if (v == 109)
-      k_window_pf<10240, AlgoFoldVar, Sink64T<true>><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, 0, n,
-                                                                                            AlgoFoldVar{}, snt);
-    else if (v == 110)
-      k_window<10224, true, AlgoCity64x2, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+    if (v == 110)
+      k_window<10224, true, AlgoCity64x2, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
           b, offsets, 0, 0, 0, n, AlgoCity64x2{}, snt);
     else
-      k_window<10224, true, AlgoCity64, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+      k_window<10224, true, AlgoCity64, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
           b, offsets, 0, 0, 0, n, AlgoCity64{}, snt);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -83,12 +75,9 @@ PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const
     else if (v == 43)
       k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 3, dev), kBlock, 0, st>>>(
           b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
-    else if (v == 45)  // windows start on a 128-B line
+    else  // 45: windows start on a 128-B line
       k_window<10224, true, AlgoLenOnly, Sink64T<true>, 2, 128><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
           b, offsets, 0, 0, 0, n, AlgoLenOnly{}, snt);
-    else
-      k_window_var<10224, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-          b, offsets, 0, n, AlgoLenOnly{}, snt);
     HIP_TRY(hipGetLastError());
     return 0;
   }

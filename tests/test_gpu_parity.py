@@ -260,11 +260,7 @@ def test_var_golden_mixed(dev, golden, oracle):
     assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
 
 
-VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2",
-               48: "k_window_rp<10224,nt>@4", 49: "k_window_rp<10224>@4",
-               100: "k_window_sorted<8,nt>@2", 101: "k_window_sorted<8>@2", 102: "k_window_sorted<4,nt>@3",
-               103: "k_window_sorted<4>@3", 104: "k_window_sorted<4>@4", 105: "k_window_sorted<16>@1",
-               106: "k_window_pf<10K,nt>@4", 107: "k_window_pf<10K>@4"}
+VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2"}
 
 
 def auto_var_kernel(total_bytes, n):
@@ -453,46 +449,32 @@ def test_device_wrappers_validate_outputs(dev):
 
 BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1000, 4096, 4097, 8192)
                 for n in (0, 1, 4095, 100003)]
-BUCKET_CASES += [(L, nr, n, v) for v in (21, 22) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192)
-                 for n in (4095, 300007)]
-BUCKET_CASES += [(L, nr, n, v) for v in (54, 58) for L in (8, 13, 16) for nr in (7, 1000, 2048)
-                 for n in (1, 16383, 16385, 1 << 20)]
-BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2049, 8192)
+BUCKET_CASES += [(L, nr, n, 21) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192) for n in (4095, 300007)]
+BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2048, 2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
 BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
 BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
                  for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
-BUCKET_CASES += [(L, nr, n, 86) for L in (8, 16, 32) for nr in (2049, 8192)
-                 for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
 
 
 def _bucket_kernel(L, nranks, variant, records=False):
-    """Product: the staged scatter for 8/16/32-B keys up to 2048 ranks, the
-    register scatter above, the generic one for other lengths.  Tuning
-    variants: 21 forces the generic-length kernel, 22 the register one, 54 the
-    gather scatter (16384-key tiles), 58 the producer/consumer one (8-B keys),
-    70 one pass at any nranks, 71 two passes from 2 ranks up, 85 the staged
-    scatter in the static tile order instead of per-XCD tickets, 83 / 87 / 89
-    the staged scatter with owner-table ranking on 8 x 16 / 4 x 16 tiles or
-    with ballots, at any nranks.  The product
-    sorts 8/16/32-B keys in two passes from 1536 / 1025 / 2049 ranks."""
+    """Product: the staged scatter for 8/16/32-B keys below the two-pass
+    threshold (1536 / 1025 / 2049 ranks), two passes from it, the generic
+    kernel for other lengths.  Tuning variants: 21 forces the generic-length
+    kernel, 70 one pass up to 2048 ranks, 71 two passes from 2 ranks up, 85
+    the staged scatter in the static tile order instead of per-XCD tickets,
+    83 / 87 / 89 the staged scatter with owner-table ranking on 8 x 16 / 4 x
+    16 tiles or with ballots, at any nranks."""
     wg = "k_bucket_scatter_wg<8>" if nranks <= 4096 else "k_bucket_scatter_wg<4>"
     if variant == 21:
         return wg
-    if variant == 22 and L in (8, 16, 32):
-        return f"k_bucket_scatter_reg<{L}B>"
-    if variant == 58 and L == 8 and nranks <= 2048:
-        return "k_bucket_scatter_pc<8B>"
-    if variant in (54, 58) and nranks <= 2048:
-        return f"k_bucket_scatter_gather<{L}B>" if L in (8, 16, 32) else "k_bucket_scatter_gather<any>"
     if L in (8, 16, 32):
         two_pass_from = {8: 1536, 16: 1025, 32: 2049}[L]
-        if (variant == 71 and nranks >= 2) or (variant != 70 and nranks >= two_pass_from):
+        one_pass = variant == 70 and nranks <= 2048
+        if (variant == 71 and nranks >= 2) or (not one_pass and nranks >= two_pass_from):
             return f"k_bucket_pass2<{L}B>"
-        if nranks > 2048:
-            return f"k_bucket_scatter_reg<{L}B>"
         # staged_shape(): owner-table ranking for array outputs from 512
         # ranks, on 8 x 16 tiles for 8/16-B keys while 81920 + 52 B per rank
         # of LDS fits a CU, else on 4 x 16 tiles while 40960 + 28 B per rank
@@ -574,11 +556,12 @@ def test_bucket_optional_outputs(dev, oracle, L):
 
 RECORD_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 7, 1000, 2049, 8192)
                 for n in (0, 1, 4095, 100003)]
-RECORD_CASES += [(L, nr, n, v) for v in (21, 22, 54, 58) for L in (8, 16, 32) for nr in (7, 1000, 2048)
-                 for n in (4097, 300007)]
-RECORD_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (7, 1000, 8192)
+RECORD_CASES += [(L, nr, n, v) for v in (21, 70, 71) for L in (8, 16, 32) for nr in (7, 1000, 2048, 8192)
                  for n in (4097, 300007)]
 RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n in (4097, (2 << 20) + 9)]
+# records switch to owner-table ranking for 16/32-B keys from 512 ranks while
+# two workgroups fit a CU (staged_shape): both edges of both thresholds
+RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]
 # 112: the r02 store order of 8-B records (header halves a staging round early)
 RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
 # records switch to owner-table ranking for 16/32-B keys from 512 ranks while
@@ -718,7 +701,7 @@ def test_cfg4_crc128_16M_full_fold(dev, folds):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-@pytest.mark.parametrize("variant", [0, 13, 48, 100, 101, 102, 103, 104, 105, 106, 107])
+@pytest.mark.parametrize("variant", [0, 13, 118])
 def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     """8.7 GB of keys: offsets far past 2^31 and 2^32 (64-bit window math)."""
     f = folds["cfg3_city64_64M_mixed"]
