@@ -13,7 +13,7 @@ constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wa
 
 // Packed 8/16/32-byte keys: each lane loads its own key (lane-adjacent rows,
 // so 8- and 16-byte keys are fully coalesced), U keys in flight per lane.
-// tools/placebench.py (interleaved A/B, r01): 8-B keys with non-temporal
+// r01 interleaved A/B (profiles/r01/placebench_*): 8-B keys with non-temporal
 // stores (+26 % on fused placement), 16-B keys with non-temporal loads and
 // stores (+6-11 %).
 template <class Algo, class Sink>
@@ -27,7 +27,7 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // run at the memory-side atomic rate (~1.3 TB/s of added bytes): 2048
     // workgroups x 1024 bins x 8 B took ~16 us of an 85-us launch; a quarter
     // as many workgroups measured +24 % (8-B keys) and +29 % (16-B keys) on
-    // 16M keys, 1024 ranks (tools/placebench.py, r01).
+    // 16M keys, 1024 ranks (profiles/r01/placebench_*).
     // (r02, tools/abbench.py place8_*: 8-B keys stream best at ONE such
     // workgroup per CU -- 0.80 of the roofline against 0.74 at two, half the
     // flushes again; 16-B keys stay at two)
@@ -69,17 +69,23 @@ static bool sink_has_hist(const Sink &s) {
 // specialised lengths when the layout allows them, else the window kernel
 // (a 64-key tile fits 12 or 16 KiB of LDS), else per-lane global reads.
 // Batches larger than this many key bytes go out as consecutive launches of
-// about this size.  One persistent launch over a multi-GiB batch streams
-// ~10 % slower than the same keys in 1 GiB launches (tools/abbench.py:
-// cfg5 = 128M x 64 B in one launch 1.814 ms; as 8 launches of 16M keys
-// 8 x 0.206 ms): over a long launch the waves drift apart, and the memory
-// the chip has in flight spreads over ever more of the buffer.
-constexpr u64 kLaunchBytes = 1ull << 30;
+// about this size.  One persistent launch over a large batch streams slower
+// than the same keys in shorter launches: over a long launch the waves drift
+// apart and the memory the chip has in flight spreads over ever more of the
+// buffer.  Interleaved A/B (tools/abbench.py, r03), 64-B keys, ms per batch:
+//   chunk               cfg5 128M keys (8 GiB)    cfg2 16M keys (1 GiB)
+//   one launch          1.806 (0.669)             0.2034 (0.742)
+//   4 GiB / 2 GiB       -     / 1.675             -
+//   1 GiB               1.614 (0.749)             0.2031
+//   512 MiB             1.579 (0.765)             0.1999 (0.755)
+//   256 MiB             1.592                     0.2011
+// (cfg3's window kernel is indifferent: 1.92 ms at 0.5-2 GiB, 1.94 in one.)
+constexpr u64 kLaunchBytes = 512ull << 20;
 static u64 launch_chunk_bytes() {
 #ifdef PDHT_HIP_TUNING
-  switch (tuning_variant()) {  // 114-118: chunk 256 MiB / 512 MiB / 2 GiB / 4 GiB / one launch
+  switch (tuning_variant()) {  // 114-118: chunk 256 MiB / 1 GiB / 2 GiB / 4 GiB / one launch
     case 114: return 256ull << 20;
-    case 115: return 512ull << 20;
+    case 115: return 1ull << 30;
     case 116: return 2ull << 30;
     case 117: return 4ull << 30;
     case 118: return ~0ull;
@@ -163,7 +169,7 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
       }
     }
 #endif
-    // measured fastest (tools/kbench.py): non-temporal loads
+    // measured fastest (profiles/r01/kbench_*): non-temporal loads
     // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU.
     // Placement with a histogram on up to 4M keys: 1024-thread workgroups, 1
     // per CU -- every workgroup ends with one device-scope atomic per bin, and

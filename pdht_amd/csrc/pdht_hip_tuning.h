@@ -12,11 +12,29 @@
 extern "C" {
 #endif
 
-/* Select an alternative kernel where one exists (0 = the product's choice):
- *   64-B keys  7 one tile of prefetch per wave, 4 WG/CU; 26 plain digest stores
- *   var keys  12 10224-B window at 4 WG/CU;   13 16 KiB window at 2 WG/CU
- *   bucketing 21 generic-length scatter;      22 register scatter
- *   host      61 chunked copy pipeline instead of zero-copy on pinned buffers
+/* Select an alternative kernel where one exists (0 = the product's choice).
+ * Every variant the sources know (DESIGN.md §4 has the measurements):
+ *   64-B keys      7  one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
+ *                 26  plain instead of non-temporal digest stores (2-6 % slower)
+ *              80/81  1024-thread transpose at 1 / 2 WG/CU (cfg1 shape)
+ *                 82  the 256-thread transpose whatever the histogram
+ *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
+ *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
+ *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
+ *                     movement alone (digest = key length): 40 as shipped,
+ *                     41 default-policy DMA, 42 plain stores, 43 3 WG/CU,
+ *                     44/45 windows on 128-B lines
+ *           110 / 111 (same entry) the window kernel hashing every key twice
+ *                     / once: what the arithmetic costs over 40
+ *   launches  114-118 key bytes per launch: 256 MiB / 1 GiB / 2 GiB / 4 GiB /
+ *                     all in one launch (product: 512 MiB)
+ *   bucketing     21  generic-length scatter for 8/16/32-B keys
+ *                 70  one pass (staged scatter) up to 2048 ranks
+ *                 71  two passes from 2 ranks up
+ *              83/87  owner-table ranking on 8 x 16 / 4 x 16 tiles, any nranks
+ *              85/89  ballot ranking, any nranks (85: static tile order)
+ *   records      112  r02 store order (header halves a staging round early)
+ *   host          61  chunked copy pipeline instead of zero-copy on pinned buffers
  * Process-wide; returns the previous value. */
 int pdht_hip_set_variant(int variant);
 /* Override the workgroups per CU of the persistent grids (0 = default).

@@ -871,8 +871,8 @@ def test_batches_capture_in_hip_graph(dev, oracle):
 
 @pytest.mark.parametrize("variant", [0, 114])
 def test_chunked_launches(dev, oracle, variant):
-    """Batches past launch_chunk_bytes() go out as consecutive launches (1 GiB
-    in the product, 256 MiB in tuning variant 114): fixed keys (digests,
+    """Batches past launch_chunk_bytes() go out as consecutive launches (512
+    MiB in the product, 256 MiB in tuning variant 114): fixed keys (digests,
     128-bit digests, fused placement with a histogram and ptl_process_t-style
     rank stride) and offset-indexed keys, ragged ends, checked against the
     oracle on samples from both sides of every chunk boundary."""
