@@ -349,6 +349,30 @@ struct Sink128T {
 typedef Sink64T<false> Sink64;
 typedef Sink128T<false> Sink128;
 
+#ifdef PDHT_HIP_TUNING
+// Calibration only: digests dropped (a kernel's loads alone).
+struct SinkNone {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64, u64 h) {
+    if (h == 0x0123456789abcdefull) out[0] = h;  // keeps the digest live, never taken
+  }
+  __device__ __forceinline__ void flush() {}
+};
+// Calibration only: every digest stored, but into the first 32 KiB of out
+// (L2-resident): the store instructions without their HBM writes.
+struct SinkSmall {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64 i, u64 h) { out[i & 4095] = h; }
+  __device__ __forceinline__ void flush() {}
+};
+#endif
+
 // The same sink with non-temporal stores (identity for other sinks).
 template <class S>
 struct NtSink {

@@ -26,6 +26,9 @@ extern "C" {
  *                     44/45 windows on 128-B lines
  *           110 / 111 (same entry) the window kernel hashing every key twice
  *                     / once: what the arithmetic costs over 40
+ *       119-121, 125  (same entry) keys read as fixed rows of the mean length,
+ *                     no offsets: nt / no / plain digest stores / plain stores
+ *                     into 32 KiB (L2-resident)
  *   launches  114-118 key bytes per launch: 256 MiB / 1 GiB / 2 GiB / 4 GiB /
  *                     all in one launch (product: 512 MiB)
  *   bucketing     21  generic-length scatter for 8/16/32-B keys

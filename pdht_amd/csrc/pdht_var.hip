@@ -34,6 +34,33 @@ PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const
   // key length): 40 as shipped; 41 default-policy DMA; 42 plain stores;
   // 43 as 40 at 3 WG/CU; 45 windows on 128-B lines
   const int v = tuning_variant();
+  if ((v >= 119 && v <= 121) || v == 125) {
+    // the window kernel's loads without the offsets: keys read as FIXED-length
+    // rows of the batch's mean length (cfg3c-like data: 136 B), 119 with nt
+    // digest stores, 120 with none, 121 plain stores, 125 plain stores into
+    // 32 KiB (L2-resident: the store instructions without the HBM writes)
+    if (n == 0) return 0;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    const uint8_t *b = static_cast<const uint8_t *>(bytes);
+    const u64 L = nbytes / n;
+    const u64 wb = ((n + 63) / 64 + 3) / 4;
+    g_kernel = "k_window<var,calib>";
+    if (v == 119)
+      k_window<10224, false, AlgoLenOnly, Sink64T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
+          b, nullptr, 0, L, L, n, AlgoLenOnly{}, Sink64T<true>{nullptr, out});
+    else if (v == 121)  // plain digest stores
+      k_window<10224, false, AlgoLenOnly, Sink64, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
+          b, nullptr, 0, L, L, n, AlgoLenOnly{}, Sink64{nullptr, out});
+    else if (v == 125)
+      k_window<10224, false, AlgoLenOnly, SinkSmall, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
+          b, nullptr, 0, L, L, n, AlgoLenOnly{}, SinkSmall{nullptr, out});
+    else
+      k_window<10224, false, AlgoLenOnly, SinkNone, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
+          b, nullptr, 0, L, L, n, AlgoLenOnly{}, SinkNone{nullptr, out});
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   if (v == 110 || v == 111) {
     // the product window kernel with CityHash64 twice per key (110) / once
     // (111): what the hash arithmetic costs over the data movement (40)

@@ -7,6 +7,7 @@ stream; every variant's output is compared with the product kernel's.
   works: cfg2 (16M x 64 B City64), cfg4 (Crc128), cfg3 (64M mixed 16..256 B),
          cfg3c (64M x 136 B through the variable-length path), cfg3fold (cfg3's
          window data movement: fold of the bytes; variant 40 = no LDS reads),
+         varfold_<L> (64M x L-B fixed keys through the var calibration entry),
          long (1M x 1 KiB Crc128), long64 (1M x 1 KiB City64),
          place (16M x 8 B, nptes 3, nranks 1024, histogram),
          bucket (16M x 8 B, 1024 ranks, keys+mbits+ptindex+index)
@@ -104,17 +105,24 @@ def workload(name, dev):
         outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
         return ((lambda: P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)),
                 (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * (8 + 8 + 8 + 4 + 4))
-    if name not in ("cfg3", "cfg3c", "cfg3fold"):
+    if name.startswith("varfold_"):  # varfold_<L>: 64M x L-B keys through the var calibration entry
+        L = int(name.split("_")[1])
+        n = 64 * M if L <= 136 else 32 * M
+        data = P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8)
+        offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device=dev)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        return (lambda: P.key_stream_var(data, offs, out=out, check=False)), (lambda: out[:1].clone()), n * (L + 16)
+    if name not in ("cfg3", "cfg3c", "cfg3fold", "cfg3cfold"):
         raise SystemExit(f"unknown work {name}")
     n = 64 * M
-    lo, hi = (136, 136) if name == "cfg3c" else (16, 256)
+    lo, hi = (136, 136) if name in ("cfg3c", "cfg3cfold") else (16, 256)
     lens = P.mixed_lengths(0x1E575EED1E575EED, 0, n, lo, hi, device=dev)
     offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     torch.cumsum(lens, 0, out=offs[1:])
     total = int(offs[-1].item())
     data = P.splitmix64_fill(SEED, 0, (total + 7) // 8, device=dev).view(torch.uint8)[:total]
     out = torch.empty(n, dtype=torch.int64, device=dev)
-    if name == "cfg3fold":  # the window kernel's data movement, hash replaced (variant 40: no LDS reads)
+    if name in ("cfg3fold", "cfg3cfold"):  # the window kernel's data movement, hash replaced (40: no LDS reads)
         return (lambda: P.key_stream_var(data, offs, out=out, check=False)), (lambda: out[:1].clone()), total + 16 * n
     return (lambda: P.city64_var_batch(data, offs, out=out, check=False)), (lambda: out.clone()), total + 16 * n
 
