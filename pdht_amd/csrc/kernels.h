@@ -208,13 +208,64 @@ struct CrcLds6Tab {
     return r;
   }
 };
+// Byte slices (slicing-by-8, 8 lookups per word) with one-instruction
+// addresses (r03).  The 6-bit form spends ~2 VALU per lookup on its address
+// (shift, mask, scale) and the long-key kernel is issue-bound (profiles/r02/sq:
+// ACTIVE + issue-stall ~75 % of wave cycles at 3 waves/SIMD), so this form
+// trades LDS space for instructions: every table is replicated for 16 lane
+// columns so a lookup is ONE v_perm_b32 that assembles the byte address
+// (x.byte_k << 8) | (64 t + 4 (lane & 15)) from the key word and a per-lane
+// constant, one ds_read_b32 and one xor.  Layout: two 64 KiB sets (bytes 0-3
+// / 4-7 of the word), each [256 byte values][4 tables][16 lane columns] of
+// u32; set 1 sits at +64 KiB, put into the address by a 0x01 byte of its
+// per-lane constants.  Lanes l and l+16 share a bank column (2-way at most
+// per 32-lane group) where the 256-entry byte tables of r01 conflicted 4.3x.
+// 128 KiB per workgroup: one 768-thread workgroup per CU.
+struct CrcLds8Tab {
+  const u32 *t;  // [2][256][4][16]
+  u32 la, lb1, lb2;
+  __device__ __forceinline__ static CrcLds8Tab make(const u32 *t) {
+    const u32 l4 = (threadIdx.x & 15) * 4;
+    return CrcLds8Tab{t, l4 * 0x01010101u + 0xC0804000u, l4 * 0x0101u + 0x00014000u,
+                      l4 * 0x0101u + 0x0001C080u};
+  }
+  __device__ __forceinline__ u32 rd(u32 a) const {
+    return *reinterpret_cast<const u32 *>(reinterpret_cast<const char *>(t) + a);
+  }
+  __device__ __forceinline__ u32 crc64(u64 x) const {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    // v_perm_b32(s0, s1, sel): selector byte j picks s1.byte[j] (0-3),
+    // s0.byte[j-4] (4-7) or 0x00 (0x0C)
+    u32 r = rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0400u)) ^ rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0501u)) ^
+            rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0602u)) ^ rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0703u));
+    r ^= rd(__builtin_amdgcn_perm(hi, lb1, 0x0C020400u)) ^ rd(__builtin_amdgcn_perm(hi, lb1, 0x0C020501u)) ^
+         rd(__builtin_amdgcn_perm(hi, lb2, 0x0C020600u)) ^ rd(__builtin_amdgcn_perm(hi, lb2, 0x0C020701u));
+    return r;
+  }
+};
+
 template <int SB>
 struct CrcLdsSlices;
 template <>
 struct CrcLdsSlices<6> {
   typedef CrcLds6Tab Tab;
   static constexpr u32 kWords = 11 * 64;
+  static constexpr int kBlock = 256, kPerCu = 8;
   __device__ static u32 word(u32 k) { return kCrc6Dev.t[k >> 6][k & 63]; }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
+};
+template <>
+struct CrcLdsSlices<8> {
+  typedef CrcLds8Tab Tab;
+  static constexpr u32 kWords = 2 * 256 * 64;
+  static constexpr int kBlock = 768, kPerCu = 1;
+  // word w = [set][byte value][table][lane column]: byte k = 4 set + table of
+  // the word, whose slicing-by-8 table is t[7 - k] (crc32c_slice8)
+  __device__ static u32 word(u32 w) {
+    const u32 k = ((w >> 14) << 2) | ((w >> 4) & 3);
+    return kCrcDev.t[7 - k][(w >> 6) & 255];
+  }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab::make(t); }
 };
 
 template <class Base, int SB = 6>
@@ -224,11 +275,11 @@ struct CrcLds : Base {
   const u32 *tab = nullptr;  // set by algo_init() inside the kernel
   template <class R>
   __device__ __forceinline__ typename Base::Out operator()(const R &r, u64 len) const {
-    typedef typename Slices::Tab Tab;
+    const auto T = Slices::make(tab);
     if constexpr (std::is_same<Base, AlgoCrc128>::value)
-      return crc128(r, len, Tab{tab});
+      return crc128(r, len, T);
     else
-      return crc128_seed(r, len, u128{this->lo, this->hi}, Tab{tab});
+      return crc128_seed(r, len, u128{this->lo, this->hi}, T);
   }
 };
 
@@ -370,6 +421,18 @@ struct SinkSmall {
   __device__ __forceinline__ void init() {}
   __device__ __forceinline__ void put(u64 i, u64 h) { out[i & 4095] = h; }
   __device__ __forceinline__ void flush() {}
+};
+// Calibration only: nt digest stores wrapped into the first 2^BITS digests
+// of out (2^BITS x 8 B: L2-sized to Infinity-Cache-sized destinations).
+template <int BITS>
+struct SinkRing {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64 i, u64 h) { st<true>(h, out + (i & ((1ull << BITS) - 1))); }
+  __device__ __forceinline__ void flush() {}
+  __host__ SinkRing shift(u64) const { return *this; }
 };
 #endif
 
@@ -686,17 +749,17 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
 // lane walks its own key straight from global memory (GlobalReader); the
 // other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
 // bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
-template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0>
-__global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ bytes,
-                                                   const u64 *__restrict__ offsets, u64 obase,
-                                                   u64 stride, u64 keylen, u64 n, Algo algo,
-                                                   Sink sink) {
+template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_global(const uint8_t *__restrict__ bytes,
+                                                  const u64 *__restrict__ offsets, u64 obase,
+                                                  u64 stride, u64 keylen, u64 n, Algo algo,
+                                                  Sink sink) {
   __shared__ u32 lds_hist[Sink::kHist];
   sink.lds_hist = lds_hist;
   algo_init(algo);
   sink.init();
-  const u64 step = (u64)gridDim.x * kBlock;
-  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) {
+  const u64 step = (u64)gridDim.x * BLOCK;
+  for (u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += step) {
     u64 st, len;
     if constexpr (VAR) {
       st = offsets[i] - obase;

@@ -192,6 +192,21 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
           k, n, algo, sink_nt);
   } else if (kShort && packed && (((keylen == 32 || keylen == 16) && al16) || (keylen == 8 && al8))) {
     if constexpr (kShort) launch_small(keylen, k, n, algo, sink, st, dev, blocks);
+  } else if constexpr (!kShort) {
+    // CRC-table algorithms (keys > 900 B: their 64-key tiles never fit a
+    // window): per-lane global reads in the workgroup shape the table form
+    // needs (byte tables: 128 KiB of LDS, one 768-thread workgroup per CU)
+    typedef typename Algo::Slices S;
+    const unsigned g = grid_for((n + S::kBlock - 1) / S::kBlock, S::kPerCu, dev);
+    if (al16 && stride % 16 == 0) {
+      g_kernel = S::kBlock == kBlock ? "k_global<fixed,a16,lines>@8" : "k_global<fixed,a16,lines,crc8,768>@1";
+      k_global<false, Algo, SinkNt, true, kLongLines, S::kBlock><<<g, S::kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+    } else {
+      g_kernel = S::kBlock == kBlock ? "k_global<fixed>@8" : "k_global<fixed,crc8,768>@1";
+      k_global<false, Algo, SinkNt, false, 0, S::kBlock><<<g, S::kBlock, 0, st>>>(k, nullptr, 0, stride,
+                                                                                  keylen, n, algo, sink_nt);
+    }
   } else {
     const u64 tiles = (n + 63) / 64;
     const u64 tile_bytes = 63 * (u64)stride + keylen + 16;  // a 64-key tile + alignment slack
@@ -202,24 +217,23 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
       // 2 WG/CU: the per-lane walks of 64 keys touch 64 lines per wave
       // instruction, and fewer waves keep more of those lines in L2 for the
       // next 16-B pieces (r02, tools/abbench.py long64: 0.575 at 2 WG/CU
-      // against 0.535 at 8); the CRC path (LDS tables) is indifferent and
-      // keeps 8.
-      constexpr int kPerCu = kShort ? 2 : 8;
+      // against 0.535 at 8)
+      constexpr int kPerCu = 2;
       if (al16 && stride % 16 == 0) {
 #ifdef PDHT_HIP_TUNING
         if (tuning_variant() == 96) {  // r02 before the line spans: 240-B / 64-B spans as the algorithm reads them
-          g_kernel = kShort ? "k_global<fixed,a16>@2" : "k_global<fixed,a16>@8";
+          g_kernel = "k_global<fixed,a16>@2";
           k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
               k, nullptr, 0, stride, keylen, n, algo, sink_nt);
           HIP_TRY(hipGetLastError());
           return 0;
         }
 #endif
-        g_kernel = kShort ? "k_global<fixed,a16,lines>@2" : "k_global<fixed,a16,lines>@8";
+        g_kernel = "k_global<fixed,a16,lines>@2";
         k_global<false, Algo, SinkNt, true, kLongLines><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, sink_nt);
       } else {
-        g_kernel = kShort ? "k_global<fixed>@2" : "k_global<fixed>@8";
+        g_kernel = "k_global<fixed>@2";
         k_global<false, Algo, SinkNt><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, sink_nt);
       }

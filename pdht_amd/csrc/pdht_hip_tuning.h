@@ -29,6 +29,11 @@ extern "C" {
  *       119-121, 125  (same entry) keys read as fixed rows of the mean length,
  *                     no offsets: nt / no / plain digest stores / plain stores
  *                     into 32 KiB (L2-resident)
+ *   cfg3 path 140-144 (pdht_city64_batch_var_dev) digests wrapped into 32 KiB
+ *                     / 2 / 8 / 32 / 128 MiB of out (wrong digests: where the
+ *                     writes land); 145-147 two-phase: 4M / 1M / 4M-key chunks
+ *                     hashed into a scratch buffer (nt / nt / plain stores),
+ *                     then copied to out
  *   launches  114-118 key bytes per launch: 256 MiB / 1 GiB / 2 GiB / 4 GiB /
  *                     all in one launch (product: 512 MiB)
  *   bucketing     21  generic-length scatter for 8/16/32-B keys

@@ -62,11 +62,14 @@ SMALL_KERNELS = {8: "k_fixed_direct<8,4,nt-store>@8", 16: "k_fixed_direct<16,2,n
 def fixed_kernel(L, stride=None, aligned=True, crc=False):
     """launch_fixed's choice for a generic length: the LDS window that holds a
     64-key tile (12 KiB or 16 KiB), else per-lane global reads (16-B loads
-    when every key starts 16-B aligned; 2 WG/CU, 8 with the LDS CRC tables)."""
+    when every key starts 16-B aligned; 2 WG/CU; with the LDS CRC byte tables
+    one 768-thread workgroup per CU)."""
     tile = 63 * (stride or L) + L + 16
     if tile > 16384:
-        g = "k_global<fixed,a16,lines>" if aligned and (stride or L) % 16 == 0 else "k_global<fixed>"
-        return g + ("@8" if crc and L > 900 else "@2")
+        a16 = aligned and (stride or L) % 16 == 0
+        if crc and L > 900:
+            return "k_global<fixed,a16,lines,crc8,768>@1" if a16 else "k_global<fixed,crc8,768>@1"
+        return ("k_global<fixed,a16,lines>" if a16 else "k_global<fixed>") + "@2"
     return "k_window<fixed,nt,16K>@2" if tile > 12288 else "k_window<fixed,nt,12K>@3"
 
 
@@ -120,7 +123,8 @@ def test_long_keys(dev, oracle, L, n):
 @pytest.mark.parametrize("L", [901, 1000, 1024, 1920, 2200, 4096])
 def test_crc128_long_keys_many_tiles(dev, oracle, L):
     """CityHashCrc256 rounds with the LDS CRC tables, every workgroup of the
-    grid busy (k_global, 8 WG/CU) and a ragged tail; seeded variant too."""
+    grid busy (k_global, one 768-thread workgroup per CU) and a ragged tail;
+    seeded variant too."""
     rng = np.random.default_rng(L)
     n = 256 * 8 * 256 + 77 if L == 901 else 70_001
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)

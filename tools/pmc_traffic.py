@@ -22,7 +22,11 @@ import os
 import statistics
 
 
-def per_launch(path, kernel, counter):
+def per_launch(path, kernel, counter, per_step=1):
+    """Median counter value per launch; with per_step > 1 (a step is several
+    launches of the kernel, e.g. 512-MiB chunks) the mean per STEP: the sum
+    over every profiled launch x per_step / launches (every profiled call of
+    the kernel is a whole step)."""
     rows = [r for r in csv.DictReader(open(path))
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
     if not rows:
@@ -30,7 +34,17 @@ def per_launch(path, kernel, counter):
     names = sorted({r["Kernel_Name"] for r in rows})
     if len(names) != 1:
         raise SystemExit(f"{kernel} matches several kernels in {path}: {names}")
-    return statistics.median(float(r["Counter_Value"]) for r in rows), len(rows), names[0]
+    # rocprofv3 may split one dispatch's counter over several rows (dimensions)
+    disp = {}
+    for j, r in enumerate(rows):
+        d = r.get("Dispatch_Id", j)
+        disp[d] = disp.get(d, 0.0) + float(r["Counter_Value"])
+    vals = list(disp.values())
+    if per_step > 1:
+        if len(vals) % per_step:
+            raise SystemExit(f"{len(vals)} launches of {kernel} are not whole steps of {per_step}")
+        return sum(vals) * per_step / len(vals), len(vals), names[0]
+    return statistics.median(vals), len(vals), names[0]
 
 
 def main():
@@ -39,6 +53,8 @@ def main():
     ap.add_argument("--keys", type=int, required=True)
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--algo-bytes-per-key", type=float, required=True)
+    ap.add_argument("--launches-per-step", type=int, default=1,
+                    help="launches of --kernel per bench step (batches split into ~512-MiB launches)")
     ap.add_argument("--dir", default="gpurun_out")
     ap.add_argument("--out", required=True)
     ap.add_argument("--fetch-dir", default=None, help="default: <dir>/pmc_FETCH_SIZE")
@@ -52,8 +68,10 @@ def main():
     nf = nw = 0
     symbols = []
     for k in a.kernel.split("|"):
-        f, nf, name = per_launch(os.path.join(fd, "run_counter_collection.csv"), k, "FETCH_SIZE")
-        w, nw, name2 = per_launch(os.path.join(wd, "run_counter_collection.csv"), k, "WRITE_SIZE")
+        f, nf, name = per_launch(os.path.join(fd, "run_counter_collection.csv"), k, "FETCH_SIZE",
+                                 a.launches_per_step)
+        w, nw, name2 = per_launch(os.path.join(wd, "run_counter_collection.csv"), k, "WRITE_SIZE",
+                                  a.launches_per_step)
         if name != name2:
             raise SystemExit(f"FETCH and WRITE passes profiled different kernels: {name} / {name2}")
         symbols.append(name)
@@ -65,7 +83,8 @@ def main():
     write = w_kib * 1024
     algo = a.algo_bytes_per_key * a.keys
     res = {"cfg": a.cfg, "kernel": a.kernel, "kernel_tag": tag, "rocprof_kernels": symbols,
-           "keys_per_launch": a.keys,
+           "keys_per_launch": a.keys,  # keys per bench step (one or more launches)
+           "launches_per_step": a.launches_per_step,
            "fetch_size_kib_raw": f_kib, "fetch_correction": 2, "write_size_kib_raw": w_kib,
            "launches_sampled": [nf, nw],
            "hbm_bytes_per_launch": int(fetch + write),
