@@ -251,19 +251,29 @@ struct CrcLdsSlices<6> {
   typedef CrcLds6Tab Tab;
   static constexpr u32 kWords = 11 * 64;
   static constexpr int kBlock = 256, kPerCu = 8;
-  __device__ static u32 word(u32 k) { return kCrc6Dev.t[k >> 6][k & 63]; }
+  __device__ static void fill(u32 *tab) {
+    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrc6Dev.t[k >> 6][k & 63];
+  }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };
 template <>
 struct CrcLdsSlices<8> {
   typedef CrcLds8Tab Tab;
   static constexpr u32 kWords = 2 * 256 * 64;
-  static constexpr int kBlock = 768, kPerCu = 1;
+  // one key per thread, not a persistent grid: with one workgroup per CU a
+  // grid-stride loop leaves the CUs whose threads hold a key fewer idle at
+  // the end of every launch; the table fill is ~3 % of a workgroup's life
+  static constexpr int kBlock = 768, kPerCu = 64;
   // word w = [set][byte value][table][lane column]: byte k = 4 set + table of
-  // the word, whose slicing-by-8 table is t[7 - k] (crc32c_slice8)
-  __device__ static u32 word(u32 w) {
-    const u32 k = ((w >> 14) << 2) | ((w >> 4) & 3);
-    return kCrcDev.t[7 - k][(w >> 6) & 255];
+  // the word, whose slicing-by-8 table is t[7 - k] (crc32c_slice8); the 16
+  // lane columns of one (set, byte, table) hold the same value, written as
+  // four 16-B stores
+  __device__ static void fill(u32 *tab) {
+    for (u32 v = threadIdx.x; v < kWords / 4; v += blockDim.x) {
+      const u32 e = v >> 2;  // (set * 256 + byte) * 4 + table
+      const u32 x = kCrcDev.t[7 - (((e >> 10) << 2) | (e & 3))][(e >> 2) & 255];
+      reinterpret_cast<u32x4 *>(tab)[v] = u32x4{x, x, x, x};
+    }
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab::make(t); }
 };
@@ -297,8 +307,8 @@ template <class Algo>
 __device__ __forceinline__ void algo_init(Algo &a) {
   if constexpr (HasCrcLds<Algo>::value) {
     typedef typename Algo::Slices S;
-    __shared__ u32 tab[S::kWords];
-    for (u32 k = threadIdx.x; k < S::kWords; k += blockDim.x) tab[k] = S::word(k);
+    __shared__ __attribute__((aligned(16))) u32 tab[S::kWords];
+    S::fill(tab);
     __syncthreads();
     a.tab = tab;
   }

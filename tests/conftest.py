@@ -11,8 +11,26 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def pytest_addoption(parser):
+    parser.addoption("--tuning", action="store_true", default=False,
+                     help="also run the tuning-build variant cases (marker 'tuning')")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+    config.addinivalue_line("markers", "tuning: a case of a tuning-build kernel variant (A/B only, never "
+                            "shipped); deselected unless --tuning is given")
+
+
+def pytest_collection_modifyitems(config, items):
+    """The tuning-build variant matrix (alternative shapes and thresholds the
+    A/B tools select) stays out of the default runs: -m gpu checks what ships."""
+    if config.getoption("--tuning"):
+        return
+    keep = [it for it in items if it.get_closest_marker("tuning") is None]
+    if len(keep) != len(items):
+        config.hook.pytest_deselected(items=[it for it in items if it.get_closest_marker("tuning")])
+        items[:] = keep
 
 
 @pytest.fixture(scope="session")

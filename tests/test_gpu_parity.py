@@ -62,14 +62,11 @@ SMALL_KERNELS = {8: "k_fixed_direct<8,4,nt-store>@8", 16: "k_fixed_direct<16,2,n
 def fixed_kernel(L, stride=None, aligned=True, crc=False):
     """launch_fixed's choice for a generic length: the LDS window that holds a
     64-key tile (12 KiB or 16 KiB), else per-lane global reads (16-B loads
-    when every key starts 16-B aligned; 2 WG/CU; with the LDS CRC byte tables
-    one 768-thread workgroup per CU)."""
+    when every key starts 16-B aligned; 2 WG/CU, 8 with the LDS CRC tables)."""
     tile = 63 * (stride or L) + L + 16
     if tile > 16384:
         a16 = aligned and (stride or L) % 16 == 0
-        if crc and L > 900:
-            return "k_global<fixed,a16,lines,crc8,768>@1" if a16 else "k_global<fixed,crc8,768>@1"
-        return ("k_global<fixed,a16,lines>" if a16 else "k_global<fixed>") + "@2"
+        return ("k_global<fixed,a16,lines>" if a16 else "k_global<fixed>") + ("@8" if crc and L > 900 else "@2")
     return "k_window<fixed,nt,16K>@2" if tile > 12288 else "k_window<fixed,nt,12K>@3"
 
 
@@ -123,8 +120,8 @@ def test_long_keys(dev, oracle, L, n):
 @pytest.mark.parametrize("L", [901, 1000, 1024, 1920, 2200, 4096])
 def test_crc128_long_keys_many_tiles(dev, oracle, L):
     """CityHashCrc256 rounds with the LDS CRC tables, every workgroup of the
-    grid busy (k_global, one 768-thread workgroup per CU) and a ragged tail;
-    seeded variant too."""
+    grid busy (k_global, 8 WG/CU) and a ragged tail; seeded variant too; the
+    tuning build's byte-table form (variant 151) on the same keys."""
     rng = np.random.default_rng(L)
     n = 256 * 8 * 256 + 77 if L == 901 else 70_001
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
@@ -135,6 +132,9 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
     got = u64(P.citycrc128_seed_batch(kd[:300], (s0, s1))).reshape(-1, 2)
     assert [tuple(int(x) for x in g) for g in got] == \
         [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:300]]
+    with P.tuning(151):
+        assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
+        assert P.last_kernel() == "k_global<fixed,a16,lines,crc8,768>@1"
 
 
 @pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 256, 300, 384, 400, 1200])
@@ -497,7 +497,12 @@ def _bucket_kernel(L, nranks, variant, records=False):
     return wg
 
 
-@pytest.mark.parametrize("L,nranks,n,variant", BUCKET_CASES)
+def _tuning_marked(cases):
+    """variant != 0 cases run only with --tuning (conftest.py)."""
+    return [c if c[-1] == 0 else pytest.param(*c, marks=pytest.mark.tuning) for c in cases]
+
+
+@pytest.mark.parametrize("L,nranks,n,variant", _tuning_marked(BUCKET_CASES))
 def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     rng = np.random.default_rng(L * 7 + nranks + n)
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
@@ -573,7 +578,7 @@ RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 <<
 RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]
 
 
-@pytest.mark.parametrize("L,nranks,n,variant", RECORD_CASES)
+@pytest.mark.parametrize("L,nranks,n,variant", _tuning_marked(RECORD_CASES))
 def test_bucket_records(dev, oracle, L, nranks, n, variant):
     """Wire records (message_t header + key) at the bucketed positions."""
     rng = np.random.default_rng(L * 11 + nranks + n)

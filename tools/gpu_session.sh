@@ -20,6 +20,8 @@ for step in "$@"; do
     tests)   timeout -k 10 900 $PYT tests -m gpu > gpurun_out/gpu_tests.log 2>&1; rc=$?
              grep -c PASSED gpurun_out/gpu_tests.log
              tail -4 gpurun_out/gpu_tests.log ;;
+    ttests)  timeout -k 10 900 $PYT tests -m "gpu and tuning" --tuning > gpurun_out/gpu_ttests.log 2>&1; rc=$?
+             tail -4 gpurun_out/gpu_ttests.log ;;
     ktests)  timeout -k 10 600 $PYT tests -m gpu -k "$K" > gpurun_out/gpu_ktests.log 2>&1; rc=$?
              tail -15 gpurun_out/gpu_ktests.log | cut -c1-300 ;;
     smoke)   timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log; rc=$?

@@ -95,6 +95,28 @@ __global__ __launch_bounds__(1024) void k_probe(unsigned long long *cyc, unsigne
       asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(a5));
       asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(a6));
       asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(a7));
+    } else if constexpr (OP == 11) {
+#define a0 c0
+#define a1 c1
+#define a2 c2
+#define a3 c3
+#define a4 c4
+#define a5 c5
+#define a6 c6
+#define a7 c7
+      CHAIN8("v_perm_b32 %0, %0, %1, %1")
+    } else if constexpr (OP == 12) {
+      CHAIN8("v_bfe_u32 %0, %0, %1, 6")
+    } else if constexpr (OP == 13) {
+      CHAIN8("v_lshl_add_u32 %0, %0, 2, %1")
+#undef a0
+#undef a1
+#undef a2
+#undef a3
+#undef a4
+#undef a5
+#undef a6
+#undef a7
     } else if constexpr (OP == 10) {  // the pk 32-bit mul on gfx950, if any: v_mul_u32_u24
       asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(c0) : "v"(b));
       asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(c1) : "v"(b));
@@ -115,7 +137,8 @@ __global__ __launch_bounds__(1024) void k_probe(unsigned long long *cyc, unsigne
 
 static const char *kNames[] = {"v_add_u32",    "v_xor_b32",       "v_mul_lo_u32",   "v_mul_hi_u32",
                                "v_alignbyte_b32", "v_alignbit_b32", "v_add3_u32",     "v_lshl_add_u64",
-                               "v_mad_u64_u32", "v_lshrrev_b64",   "v_mul_u32_u24"};
+                               "v_mad_u64_u32", "v_lshrrev_b64",   "v_mul_u32_u24",  "v_perm_b32",
+                               "v_bfe_u32",     "v_lshl_add_u32"};
 
 template <int OP>
 static void run(int cus, int w_per_simd, unsigned long long *d_cyc, unsigned *d_sink) {
@@ -156,6 +179,9 @@ int main() {
     run<8>(cus, w, d_cyc, d_sink);
     run<9>(cus, w, d_cyc, d_sink);
     run<10>(cus, w, d_cyc, d_sink);
+    run<11>(cus, w, d_cyc, d_sink);
+    run<12>(cus, w, d_cyc, d_sink);
+    run<13>(cus, w, d_cyc, d_sink);
   }
   return 0;
 }
