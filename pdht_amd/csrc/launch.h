@@ -104,7 +104,12 @@ template <class Algo, class Sink>
 static int launch_fixed(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
                         hipStream_t st) {
   const u64 per = std::max<u64>(1, launch_chunk_bytes() / std::max<u64>(stride, 1));
-  if (n <= per || stride == 0) return launch_fixed_one(keys, stride, keylen, n, algo, sink, st);
+  // Keys too long for a 64-key window (k_global: per-lane walks, compute-
+  // heavy) go out in ONE launch: every launch ends in a tail of idle CUs, and
+  // these kernels gain nothing from short launches (r03 A/B, 1M x 1 KiB:
+  // Crc128 0.544 -> 0.566, CityHash64 0.659 -> 0.672; profiles/r03/ab).
+  const bool long_keys = 63 * (u64)stride + keylen + 16 > 16384;
+  if (n <= per || stride == 0 || long_keys) return launch_fixed_one(keys, stride, keylen, n, algo, sink, st);
   const u64 step = (per + 4095) & ~(u64)4095;  // whole 64-key tiles (and 4096-key blocks)
   const char *tag = "";
   for (u64 k0 = 0; k0 < n; k0 += step) {
