@@ -244,6 +244,27 @@ struct CrcLds8Tab {
   }
 };
 
+#ifdef PDHT_HIP_TUNING
+// Plain slicing-by-8 byte tables (8 KiB, one copy) with each address one
+// SDWA shift of the key word's byte: 8 lookups of 2 VOP2 instructions per
+// word, against the 6-bit form's 11 of ~3; 256-entry tables conflict in LDS.
+struct CrcLdsByteTab {
+  const u32 *t;  // [8][256], table k for byte k of the word (= slice8 t[7-k])
+  __device__ __forceinline__ u32 rd(u32 k, u32 b) const { return t[256 * k + b]; }
+  __device__ __forceinline__ u32 crc64(u64 x) const {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    return rd(0, lo & 255) ^ rd(1, (lo >> 8) & 255) ^ rd(2, (lo >> 16) & 255) ^ rd(3, lo >> 24) ^
+           rd(4, hi & 255) ^ rd(5, (hi >> 8) & 255) ^ rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24);
+  }
+};
+// Timing only: the CRC-32C of a word replaced by a fold (no table lookups):
+// what the lookups cost the long-key kernel (wrong digests).
+struct CrcNullTab {
+  const u32 *t;
+  __device__ __forceinline__ u32 crc64(u64 x) const { return (u32)x ^ (u32)(x >> 32) ^ t[0]; }
+};
+#endif
+
 template <int SB>
 struct CrcLdsSlices;
 template <>
@@ -256,6 +277,30 @@ struct CrcLdsSlices<6> {
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };
+#ifdef PDHT_HIP_TUNING
+template <>
+struct CrcLdsSlices<0> {  // CrcNullTab: the 6-bit form's launch shape, no lookups
+  typedef CrcNullTab Tab;
+  static constexpr u32 kWords = 64;
+  static constexpr int kBlock = 256, kPerCu = 8;
+  __device__ static void fill(u32 *tab) {
+    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = 0;
+  }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
+};
+#endif
+#ifdef PDHT_HIP_TUNING
+template <>
+struct CrcLdsSlices<7> {  // CrcLdsByteTab in the 6-bit form's launch shape
+  typedef CrcLdsByteTab Tab;
+  static constexpr u32 kWords = 8 * 256;
+  static constexpr int kBlock = 256, kPerCu = 8;
+  __device__ static void fill(u32 *tab) {
+    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrcDev.t[7 - (k >> 8)][k & 255];
+  }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
+};
+#endif
 template <>
 struct CrcLdsSlices<8> {
   typedef CrcLds8Tab Tab;
@@ -759,8 +804,8 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
 // lane walks its own key straight from global memory (GlobalReader); the
 // other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
 // bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
-template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0, int BLOCK = kBlock>
-__global__ __launch_bounds__(BLOCK) void k_global(const uint8_t *__restrict__ bytes,
+template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0, int BLOCK = kBlock, int WPE = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_global(const uint8_t *__restrict__ bytes,
                                                   const u64 *__restrict__ offsets, u64 obase,
                                                   u64 stride, u64 keylen, u64 n, Algo algo,
                                                   Sink sink) {

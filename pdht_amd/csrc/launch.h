@@ -203,6 +203,17 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
     // needs (byte tables: 128 KiB of LDS, one 768-thread workgroup per CU)
     typedef typename Algo::Slices S;
     const unsigned g = grid_for((n + S::kBlock - 1) / S::kBlock, S::kPerCu, dev);
+#ifdef PDHT_HIP_TUNING
+    if constexpr (S::kBlock == kBlock) {
+      if (tuning_variant() == 152 && al16 && stride % 16 == 0) {  // at most 128 VGPRs: 4 waves per SIMD
+        g_kernel = "k_global<fixed,a16,lines,wpe4>@8";
+        k_global<false, Algo, SinkNt, true, kLongLines, S::kBlock, 4><<<g, S::kBlock, 0, st>>>(
+            k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
+    }
+#endif
     if (al16 && stride % 16 == 0) {
       g_kernel = S::kBlock == kBlock ? "k_global<fixed,a16,lines>@8" : "k_global<fixed,a16,lines,crc8,768>@1";
       k_global<false, Algo, SinkNt, true, kLongLines, S::kBlock><<<g, S::kBlock, 0, st>>>(

@@ -20,6 +20,9 @@ extern "C" {
  *                 82  the 256-thread transpose whatever the histogram
  *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
  *                151  CRC-32C byte tables, v_perm addresses, 768-thread workgroups
+ *                152  the 6-bit form held to 128 VGPRs (4 waves per SIMD; spills)
+ *                153  timing only: CRC lookups replaced by a fold (wrong digests)
+ *                154  plain slicing-by-8 tables (8 KiB), one SDWA shift per lookup address
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,

@@ -63,6 +63,30 @@ __global__ __launch_bounds__(256) void rd(const u32x4 *__restrict__ p, u64 ntile
   if (s == 0x123456789ull) out[0] = s;  // keep the loads
 }
 
+// Per-lane walk (the long-key kernels' shape): a wave takes 64 rows of L
+// bytes, lane l walks row l in spans of P 16-B pieces (P dwordx4 loads in
+// flight per lane), every wave-instruction touching 64 different lines.
+template <int L, int P>
+__global__ __launch_bounds__(256) void walk(const u32x4 *__restrict__ p, u64 nrows, u64 *out) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 wave = (u64)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const u64 nw = (u64)gridDim.x * 4;
+  u32x4 acc = {0, 0, 0, 0};
+  for (u64 t = wave; t * 64 < nrows; t += nw) {
+    const u32x4 *q = p + (t * 64 + lane) * (L / 16);
+#pragma unroll 1
+    for (int o = 0; o < L / 16; o += P) {
+      u32x4 v[P];
+#pragma unroll
+      for (int j = 0; j < P; ++j) v[j] = q[o + j];
+#pragma unroll
+      for (int j = 0; j < P; ++j) acc ^= v[j] * 3u;
+    }
+  }
+  u64 s = ((u64)(acc.x ^ acc.z) << 32) | (acc.y ^ acc.w);
+  if (s == 0x123456789ull) out[0] = s;
+}
+
 template <bool NT>
 __global__ __launch_bounds__(256) void rdpf(const u32x4 *__restrict__ p, u64 ntile, u64 *out) {
   const u32 lane = threadIdx.x & 63;
@@ -315,6 +339,14 @@ int main(int argc, char **argv) {
       ADD("kvreg<2,nt>", pc, kvb, (kvreg<2, true><<<g, 256>>>(p4, ntile, out)));
       ADD("kvreg<2,plain>", pc, kvb, (kvreg<2, false><<<g, 256>>>(p4, ntile, out)));
       ADD("kvreg<3,nt>", pc, kvb, (kvreg<3, true><<<g, 256>>>(p4, ntile, out)));
+    }
+  } else if (which == "walk") {  // per-lane walks over 1 KiB rows vs the coalesced read
+    const u64 rows = bytes / 1024;
+    for (int pc : {2, 4, 8}) {
+      ADD("rd<4,plain>", pc, rdb, rd<4, false><<<g, 256>>>(p4, ntile, out));
+      ADD("walk<1024,16>", pc, rdb, (walk<1024, 16><<<g, 256>>>(p4, rows, out)));
+      ADD("walk<1024,8>", pc, rdb, (walk<1024, 8><<<g, 256>>>(p4, rows, out)));
+      ADD("walk<1024,4>", pc, rdb, (walk<1024, 4><<<g, 256>>>(p4, rows, out)));
     }
   } else {  // "write": store shapes next to the 64-B key stream
     u32x4 *w4 = reinterpret_cast<u32x4 *>(out + 2);  // 16-B aligned
