@@ -91,15 +91,20 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // slower: every 16-B piece refetched its line -- and CityHash128's 16-B
 // shifted loop on line spans -- 5 % slower; both removed in r03.)
 constexpr int kLongLines = 5;
+// NT = kLongStream (r03): CityHashCrc256Long's chunks read line by line, one
+// 128-B line in flight per lane (crc_stream_line, city_core.h); CityHash64
+// as with kLongLines.
+constexpr int kLongStream = 6;
 template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
   static constexpr bool kLines = NT == kLongLines;
-  static constexpr bool kPairs = NT == kLongLines;
+  static constexpr bool kPairs = NT == kLongLines || NT == kLongStream;
+  static constexpr bool kStream = NT == kLongStream;
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
-    if constexpr (A16 && NT == kLongLines && N % 8 == 0 && N % 16 != 0) {
+    if constexpr (A16 && (NT == kLongLines || NT == kLongStream) && N % 8 == 0 && N % 16 != 0) {
       if ((a & 7) == 0) {
         typedef u32 u32x2 __attribute__((ext_vector_type(2)));
         typedef const __attribute__((address_space(1))) u32x2 gu32x2;

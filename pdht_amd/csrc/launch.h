@@ -214,6 +214,15 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
       }
     }
 #endif
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 155 && al16 && stride % 16 == 0) {  // CRC chunks streamed line by line
+      g_kernel = S::kBlock == kBlock ? "k_global<fixed,a16,stream>@8" : "k_global<fixed,a16,stream,crc8,768>@1";
+      k_global<false, Algo, SinkNt, true, kLongStream, S::kBlock><<<g, S::kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+#endif
     if (al16 && stride % 16 == 0) {
       g_kernel = S::kBlock == kBlock ? "k_global<fixed,a16,lines>@8" : "k_global<fixed,a16,lines,crc8,768>@1";
       k_global<false, Algo, SinkNt, true, kLongLines, S::kBlock><<<g, S::kBlock, 0, st>>>(

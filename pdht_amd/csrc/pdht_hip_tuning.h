@@ -23,6 +23,7 @@ extern "C" {
  *                152  the 6-bit form held to 128 VGPRs (4 waves per SIMD; spills)
  *                153  timing only: CRC lookups replaced by a fold (wrong digests)
  *                154  plain slicing-by-8 tables (8 KiB), one SDWA shift per lookup address
+ *                155  CRC-256 chunks streamed line by line (one 128-B line in flight per lane)
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,

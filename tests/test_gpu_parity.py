@@ -132,6 +132,9 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
     got = u64(P.citycrc128_seed_batch(kd[:300], (s0, s1))).reshape(-1, 2)
     assert [tuple(int(x) for x in g) for g in got] == \
         [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:300]]
+    with P.tuning(155):  # CRC chunks streamed line by line
+        assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
+        assert P.last_kernel() == ("k_global<fixed,a16,stream>@8" if L % 16 == 0 else fixed_kernel(L, crc=True))
     with P.tuning(151):
         assert (u64(P.citycrc128_batch(kd)) == oracle.city128_fixed(k, crc=True)).all()
         assert P.last_kernel() == ("k_global<fixed,a16,lines,crc8,768>@1" if L % 16 == 0
