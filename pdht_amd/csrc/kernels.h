@@ -95,6 +95,9 @@ constexpr int kLongLines = 5;
 // 128-B line in flight per lane (crc_stream_line, city_core.h); CityHash64
 // as with kLongLines.
 constexpr int kLongStream = 6;
+// NT = kVarWide (r03, variable-length keys read per lane from global memory):
+// the dword runs of unaligned spans as 16-B loads at 4-B alignment.
+constexpr int kVarWide = 7;
 template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
   static constexpr bool kLines = NT == kLongLines;
@@ -137,8 +140,26 @@ struct GlobalReaderT {
     gu32 *q = reinterpret_cast<gu32 *>(a & ~(uintptr_t)3);
     const u32 r = (u32)(a & 3);
     u32 raw[N / 4 + 1];
+    if constexpr (NT == kVarWide && N >= 16) {
+      // the dword run as 16-B loads at 4-B alignment (one global_load_dwordx4
+      // per 4 dwords; a piece may straddle two lines)
+      typedef u32 u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+      typedef const __attribute__((address_space(1))) u32x4a gu32x4a;
+      gu32x4a *q4 = reinterpret_cast<gu32x4a *>(q);
 #pragma unroll
-    for (int j = 0; j < N / 4; ++j) raw[j] = q[j];
+      for (int j = 0; j < N / 16; ++j) {
+        const u32x4a v = q4[j];
+        raw[4 * j] = v.x;
+        raw[4 * j + 1] = v.y;
+        raw[4 * j + 2] = v.z;
+        raw[4 * j + 3] = v.w;
+      }
+#pragma unroll
+      for (int j = 4 * (N / 16); j < N / 4; ++j) raw[j] = q[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < N / 4; ++j) raw[j] = q[j];
+    }
     raw[N / 4] = r ? q[N / 4] : 0u;
     Words<N / 4> w;
 #pragma unroll

@@ -324,6 +324,18 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
 #ifdef PDHT_HIP_TUNING
   if (tuning_variant() == 12) wide = false;
   if (tuning_variant() == 13) wide = true;
+  if (tuning_variant() == 156 || tuning_variant() == 157) {  // no LDS window: per-lane reads from global memory
+    const bool w4 = tuning_variant() == 156;
+    g_kernel = w4 ? "k_global<var,wide>@8" : "k_global<var>@8";
+    if (w4)
+      k_global<true, Algo, SinkNt, false, kVarWide><<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, st>>>(
+          b, offsets, obase, 0, 0, n, algo, sink_nt);
+    else
+      k_global<true, Algo, SinkNt><<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, st>>>(
+          b, offsets, obase, 0, 0, n, algo, sink_nt);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
 #endif
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";

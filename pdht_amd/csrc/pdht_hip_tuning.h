@@ -25,6 +25,8 @@ extern "C" {
  *                154  plain slicing-by-8 tables (8 KiB), one SDWA shift per lookup address
  *                155  CRC-256 chunks streamed line by line (one 128-B line in flight per lane)
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
+ *            156 / 157 no window: per-lane reads from global memory (16-B loads at
+ *                     4-B alignment / dword loads), 8 WG/CU
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,
  *                     41 default-policy DMA, 42 plain stores, 43 3 WG/CU,
