@@ -535,43 +535,6 @@ template <class R>
 struct ReaderLines<R, decltype((void)R::kLines)> {
   static constexpr bool value = R::kLines;
 };
-template <class R, class = void>
-struct ReaderStream {
-  static constexpr bool value = false;
-};
-template <class R>
-struct ReaderStream<R, decltype((void)R::kStream)> {
-  static constexpr bool value = R::kStream;
-};
-
-// Line-stream form of CityHashCrc256Long's main loop (readers that set
-// kStream; r03).  The 6 * blocks chunks of [0, 240 * blocks) are one stream of
-// 40-B chunks with alternating (mult, flip) -- (1, 1) for even chunk g,
-// (k0, 0) for odd g, since a block holds an even number of chunks -- so the
-// block boundaries do not matter to the mixing.  The stream is read as whole
-// 128-B lines of the key, ONE line in flight per lane while the previous one
-// is mixed (tools/hbm_probe walk: a lane walking its row one 128-B line per
-// span streams like a coalesced read; two lines per span, as the 240-B
-// blocks load, 30 % slower).  Lines alternate between two register buffers;
-// a chunk starting in line m may run into line m+1 (at offsets 120, 112,
-// 104, 96 of the 5-line / 16-chunk period) and is mixed last, after line
-// m+1 has arrived.  Lines are loaded only while they lie wholly inside the
-// key; the chunks left after the last such line are loaded at once.
-template <int P, bool ODD, class Chunk>
-PDHT_HD void crc_stream_line(const Words<32> &A, const Words<32> &B, u64 gbase, u64 G, Chunk &&chunk) {
-  const Words<32> &cur = ODD ? B : A;
-  const Words<32> &nxt = ODD ? A : B;
-  constexpr int J0 = (128 * P + 39) / 40, J1 = (128 * (P + 1) + 39) / 40;
-#pragma unroll
-  for (int j = J0; j < J1; ++j) {
-    if (gbase + (u64)j >= G) return;  // uniform for fixed-length batches
-    const int d = (40 * j - 128 * P) / 4;  // first dword of the chunk in cur
-    auto dw = [&](int k) -> u32 { return d + k < 32 ? cur.d[d + k < 32 ? d + k : 0] : nxt.d[d + k >= 32 ? d + k - 32 : 0]; };
-    auto w = [&](int i) -> u64 { return ((u64)dw(2 * i + 1) << 32) | dw(2 * i); };
-    chunk(w(0), w(1), w(2), w(3), w(4), (j & 1) ? kK0 : (u64)1, (j & 1) ? 0u : 1u);
-  }
-}
-
 // Block at key offset o (o = 240k, C = 16 * (k mod 8) bytes of it carried):
 // loads [o + C, o + C + LB), LB = 256 (128 when C = 112).
 template <int C, class R>
@@ -605,30 +568,16 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
   Words<60> q;
   Words<28> carry;
   constexpr bool kLn = ReaderLines<R>::value;
-  constexpr bool kSt = ReaderStream<R>::value;
   auto line_end = [](u64 k) { return 240 * k + 16 * (k & 7) + ((k & 7) == 7 ? 128 : 256); };
-  const bool stream = kSt && len >= 256;  // lines 0 and 1 lie inside the key
-  Words<32> LA, LB;
-  u64 a, b, c, d, e;
-  if (stream) {
-    LA = s.template span<128>(0);
-    LB = s.template span<128>(128);
-    a = LA.w64(56) + kK0;
-    b = LA.w64(96) + kK0;
-    c = out[0] = mix16(b, len);
-    d = out[1] = LA.w64(120) * kK0 + len;
-    e = LB.w64(56) + seed;
-  } else {
-    if (kLn && line_end(0) <= len)
-      crc_block_lines<0>(s, 0, carry, q);
-    else
-      q = s.template span<240>(0);  // block 0 (len >= 240)
-    a = q.w64(56) + kK0;
-    b = q.w64(96) + kK0;
-    c = out[0] = mix16(b, len);
-    d = out[1] = q.w64(120) * kK0 + len;
-    e = q.w64(184) + seed;
-  }
+  if (kLn && line_end(0) <= len)
+    crc_block_lines<0>(s, 0, carry, q);
+  else
+    q = s.template span<240>(0);  // block 0 (len >= 240)
+  u64 a = q.w64(56) + kK0;
+  u64 b = q.w64(96) + kK0;
+  u64 c = out[0] = mix16(b, len);
+  u64 d = out[1] = q.w64(120) * kK0 + len;
+  u64 e = q.w64(184) + seed;
   u64 f = seed, g = 0, h = 0, i = 0, j = 0;
   u64 t = c + d;
   u32 o = 0;
@@ -652,54 +601,7 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
   };
   const u64 blocks = len / 240;
   u64 rest = len - blocks * 240;
-  if constexpr (kSt) {
-    if (stream) {
-      const u64 G = 6 * blocks;                // chunks of the main loop
-      const u64 nfull = len >> 7;              // lines wholly inside the key
-      auto mixc = [&](u64 w0, u64 w1, u64 w2, u64 w3, u64 w4, u64 mult, u32 flip) {
-        chunk(w0, w1, w2, w3, w4, mult, flip);
-      };
-      // line m is mixed while line m+1 is inside the key (its spill chunk)
-      u64 m = 0;
-      for (; m + 1 < nfull && 16 * (m / 5) + (128 * (m % 5) + 39) / 40 < G; ++m) {
-        const u64 gb = 16 * (m / 5);
-        switch (m % 10) {  // line of the 5-line period, and which buffer holds it
-          case 0: crc_stream_line<0, false>(LA, LB, gb, G, mixc); break;
-          case 1: crc_stream_line<1, true>(LA, LB, gb, G, mixc); break;
-          case 2: crc_stream_line<2, false>(LA, LB, gb, G, mixc); break;
-          case 3: crc_stream_line<3, true>(LA, LB, gb, G, mixc); break;
-          case 4: crc_stream_line<4, false>(LA, LB, gb, G, mixc); break;
-          case 5: crc_stream_line<0, true>(LA, LB, gb, G, mixc); break;
-          case 6: crc_stream_line<1, false>(LA, LB, gb, G, mixc); break;
-          case 7: crc_stream_line<2, true>(LA, LB, gb, G, mixc); break;
-          case 8: crc_stream_line<3, false>(LA, LB, gb, G, mixc); break;
-          default: crc_stream_line<4, true>(LA, LB, gb, G, mixc); break;
-        }
-        // the buffer of line m is free: line m+2 goes into it
-        if (m + 2 < nfull) {
-          if (m & 1)
-            LB = s.template span<128>((u32)(m + 2) << 7);
-          else
-            LA = s.template span<128>((u32)(m + 2) << 7);
-        }
-      }
-      // main-loop chunks after the streamed lines (at most 7: they start in
-      // the last two lines of the key), every load issued before the first mix
-      u64 g0 = 16 * (m / 5) + (128 * (m % 5) + 39) / 40;
-      if (g0 > G) g0 = G;
-      Words<10> tr[7];
-#pragma unroll
-      for (int k = 0; k < 7; ++k)
-        if (g0 + k < G) tr[k] = s.template span<40>((u32)(40 * (g0 + k)));
-#pragma unroll
-      for (int k = 0; k < 7; ++k)
-        if (g0 + k < G)
-          chunk(tr[k].w64(0), tr[k].w64(8), tr[k].w64(16), tr[k].w64(24), tr[k].w64(32),
-                ((g0 + k) & 1) ? kK0 : (u64)1, ((g0 + k) & 1) ? 0u : 1u);
-      o = (u32)(240 * blocks);
-    }
-  }
-  for (u64 k = 0; !stream && k < blocks; ++k) {
+  for (u64 k = 0; k < blocks; ++k) {
     // (prefetching the next block as well measured equal, r02: 165 VGPRs)
     if (k) {
       if (kLn && line_end(k) <= len)  // uniform for fixed-length batches

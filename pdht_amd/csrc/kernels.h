@@ -91,23 +91,15 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // slower: every 16-B piece refetched its line -- and CityHash128's 16-B
 // shifted loop on line spans -- 5 % slower; both removed in r03.)
 constexpr int kLongLines = 5;
-// NT = kLongStream (r03): CityHashCrc256Long's chunks read line by line, one
-// 128-B line in flight per lane (crc_stream_line, city_core.h); CityHash64
-// as with kLongLines.
-constexpr int kLongStream = 6;
-// NT = kVarWide (r03, variable-length keys read per lane from global memory):
-// the dword runs of unaligned spans as 16-B loads at 4-B alignment.
-constexpr int kVarWide = 7;
 template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
   static constexpr bool kLines = NT == kLongLines;
-  static constexpr bool kPairs = NT == kLongLines || NT == kLongStream;
-  static constexpr bool kStream = NT == kLongStream;
+  static constexpr bool kPairs = NT == kLongLines;
   const uint8_t *p;
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
-    if constexpr (A16 && (NT == kLongLines || NT == kLongStream) && N % 8 == 0 && N % 16 != 0) {
+    if constexpr (A16 && NT == kLongLines && N % 8 == 0 && N % 16 != 0) {
       if ((a & 7) == 0) {
         typedef u32 u32x2 __attribute__((ext_vector_type(2)));
         typedef const __attribute__((address_space(1))) u32x2 gu32x2;
@@ -140,26 +132,8 @@ struct GlobalReaderT {
     gu32 *q = reinterpret_cast<gu32 *>(a & ~(uintptr_t)3);
     const u32 r = (u32)(a & 3);
     u32 raw[N / 4 + 1];
-    if constexpr (NT == kVarWide && N >= 16) {
-      // the dword run as 16-B loads at 4-B alignment (one global_load_dwordx4
-      // per 4 dwords; a piece may straddle two lines)
-      typedef u32 u32x4a __attribute__((ext_vector_type(4), aligned(4)));
-      typedef const __attribute__((address_space(1))) u32x4a gu32x4a;
-      gu32x4a *q4 = reinterpret_cast<gu32x4a *>(q);
 #pragma unroll
-      for (int j = 0; j < N / 16; ++j) {
-        const u32x4a v = q4[j];
-        raw[4 * j] = v.x;
-        raw[4 * j + 1] = v.y;
-        raw[4 * j + 2] = v.z;
-        raw[4 * j + 3] = v.w;
-      }
-#pragma unroll
-      for (int j = 4 * (N / 16); j < N / 4; ++j) raw[j] = q[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < N / 4; ++j) raw[j] = q[j];
-    }
+    for (int j = 0; j < N / 4; ++j) raw[j] = q[j];
     raw[N / 4] = r ? q[N / 4] : 0u;
     Words<N / 4> w;
 #pragma unroll
@@ -234,55 +208,7 @@ struct CrcLds6Tab {
     return r;
   }
 };
-// Byte slices (slicing-by-8, 8 lookups per word) with one-instruction
-// addresses (r03).  The 6-bit form spends ~2 VALU per lookup on its address
-// (shift, mask, scale) and the long-key kernel is issue-bound (profiles/r02/sq:
-// ACTIVE + issue-stall ~75 % of wave cycles at 3 waves/SIMD), so this form
-// trades LDS space for instructions: every table is replicated for 16 lane
-// columns so a lookup is ONE v_perm_b32 that assembles the byte address
-// (x.byte_k << 8) | (64 t + 4 (lane & 15)) from the key word and a per-lane
-// constant, one ds_read_b32 and one xor.  Layout: two 64 KiB sets (bytes 0-3
-// / 4-7 of the word), each [256 byte values][4 tables][16 lane columns] of
-// u32; set 1 sits at +64 KiB, put into the address by a 0x01 byte of its
-// per-lane constants.  Lanes l and l+16 share a bank column (2-way at most
-// per 32-lane group) where the 256-entry byte tables of r01 conflicted 4.3x.
-// 128 KiB per workgroup: one 768-thread workgroup per CU.
-struct CrcLds8Tab {
-  const u32 *t;  // [2][256][4][16]
-  u32 la, lb1, lb2;
-  __device__ __forceinline__ static CrcLds8Tab make(const u32 *t) {
-    const u32 l4 = (threadIdx.x & 15) * 4;
-    return CrcLds8Tab{t, l4 * 0x01010101u + 0xC0804000u, l4 * 0x0101u + 0x00014000u,
-                      l4 * 0x0101u + 0x0001C080u};
-  }
-  __device__ __forceinline__ u32 rd(u32 a) const {
-    return *reinterpret_cast<const u32 *>(reinterpret_cast<const char *>(t) + a);
-  }
-  __device__ __forceinline__ u32 crc64(u64 x) const {
-    const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    // v_perm_b32(s0, s1, sel): selector byte j picks s1.byte[j] (0-3),
-    // s0.byte[j-4] (4-7) or 0x00 (0x0C)
-    u32 r = rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0400u)) ^ rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0501u)) ^
-            rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0602u)) ^ rd(__builtin_amdgcn_perm(lo, la, 0x0C0C0703u));
-    r ^= rd(__builtin_amdgcn_perm(hi, lb1, 0x0C020400u)) ^ rd(__builtin_amdgcn_perm(hi, lb1, 0x0C020501u)) ^
-         rd(__builtin_amdgcn_perm(hi, lb2, 0x0C020600u)) ^ rd(__builtin_amdgcn_perm(hi, lb2, 0x0C020701u));
-    return r;
-  }
-};
-
 #ifdef PDHT_HIP_TUNING
-// Plain slicing-by-8 byte tables (8 KiB, one copy) with each address one
-// SDWA shift of the key word's byte: 8 lookups of 2 VOP2 instructions per
-// word, against the 6-bit form's 11 of ~3; 256-entry tables conflict in LDS.
-struct CrcLdsByteTab {
-  const u32 *t;  // [8][256], table k for byte k of the word (= slice8 t[7-k])
-  __device__ __forceinline__ u32 rd(u32 k, u32 b) const { return t[256 * k + b]; }
-  __device__ __forceinline__ u32 crc64(u64 x) const {
-    const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    return rd(0, lo & 255) ^ rd(1, (lo >> 8) & 255) ^ rd(2, (lo >> 16) & 255) ^ rd(3, lo >> 24) ^
-           rd(4, hi & 255) ^ rd(5, (hi >> 8) & 255) ^ rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24);
-  }
-};
 // Timing only: the CRC-32C of a word replaced by a fold (no table lookups):
 // what the lookups cost the long-key kernel (wrong digests).
 struct CrcNullTab {
@@ -297,7 +223,6 @@ template <>
 struct CrcLdsSlices<6> {
   typedef CrcLds6Tab Tab;
   static constexpr u32 kWords = 11 * 64;
-  static constexpr int kBlock = 256, kPerCu = 8;
   __device__ static void fill(u32 *tab) {
     for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrc6Dev.t[k >> 6][k & 63];
   }
@@ -308,47 +233,12 @@ template <>
 struct CrcLdsSlices<0> {  // CrcNullTab: the 6-bit form's launch shape, no lookups
   typedef CrcNullTab Tab;
   static constexpr u32 kWords = 64;
-  static constexpr int kBlock = 256, kPerCu = 8;
   __device__ static void fill(u32 *tab) {
     for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = 0;
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };
 #endif
-#ifdef PDHT_HIP_TUNING
-template <>
-struct CrcLdsSlices<7> {  // CrcLdsByteTab in the 6-bit form's launch shape
-  typedef CrcLdsByteTab Tab;
-  static constexpr u32 kWords = 8 * 256;
-  static constexpr int kBlock = 256, kPerCu = 8;
-  __device__ static void fill(u32 *tab) {
-    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrcDev.t[7 - (k >> 8)][k & 255];
-  }
-  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
-};
-#endif
-template <>
-struct CrcLdsSlices<8> {
-  typedef CrcLds8Tab Tab;
-  static constexpr u32 kWords = 2 * 256 * 64;
-  // one key per thread, not a persistent grid: with one workgroup per CU a
-  // grid-stride loop leaves the CUs whose threads hold a key fewer idle at
-  // the end of every launch; the table fill is ~3 % of a workgroup's life
-  static constexpr int kBlock = 768, kPerCu = 64;
-  // word w = [set][byte value][table][lane column]: byte k = 4 set + table of
-  // the word, whose slicing-by-8 table is t[7 - k] (crc32c_slice8); the 16
-  // lane columns of one (set, byte, table) hold the same value, written as
-  // four 16-B stores
-  __device__ static void fill(u32 *tab) {
-    for (u32 v = threadIdx.x; v < kWords / 4; v += blockDim.x) {
-      const u32 e = v >> 2;  // (set * 256 + byte) * 4 + table
-      const u32 x = kCrcDev.t[7 - (((e >> 10) << 2) | (e & 3))][(e >> 2) & 255];
-      reinterpret_cast<u32x4 *>(tab)[v] = u32x4{x, x, x, x};
-    }
-  }
-  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab::make(t); }
-};
-
 template <class Base, int SB = 6>
 struct CrcLds : Base {
   static constexpr bool kCrcLds = true;
@@ -830,8 +720,8 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
 // lane walks its own key straight from global memory (GlobalReader); the
 // other lanes' reads of the same 128-B lines arrive through L2.  VAR: key i =
 // bytes[offsets[i]-obase, offsets[i+1]-obase); else bytes[i*stride, +keylen).
-template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0, int BLOCK = kBlock, int WPE = 1>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_global(const uint8_t *__restrict__ bytes,
+template <bool VAR, class Algo, class Sink, bool A16 = false, int NT = 0>
+__global__ __launch_bounds__(kBlock) void k_global(const uint8_t *__restrict__ bytes,
                                                   const u64 *__restrict__ offsets, u64 obase,
                                                   u64 stride, u64 keylen, u64 n, Algo algo,
                                                   Sink sink) {
@@ -839,8 +729,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
   sink.lds_hist = lds_hist;
   algo_init(algo);
   sink.init();
-  const u64 step = (u64)gridDim.x * BLOCK;
-  for (u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x; i < n; i += step) {
+  const u64 step = (u64)gridDim.x * kBlock;
+  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) {
     u64 st, len;
     if constexpr (VAR) {
       st = offsets[i] - obase;

@@ -199,38 +199,16 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
     if constexpr (kShort) launch_small(keylen, k, n, algo, sink, st, dev, blocks);
   } else if constexpr (!kShort) {
     // CRC-table algorithms (keys > 900 B: their 64-key tiles never fit a
-    // window): per-lane global reads in the workgroup shape the table form
-    // needs (byte tables: 128 KiB of LDS, one 768-thread workgroup per CU)
-    typedef typename Algo::Slices S;
-    const unsigned g = grid_for((n + S::kBlock - 1) / S::kBlock, S::kPerCu, dev);
-#ifdef PDHT_HIP_TUNING
-    if constexpr (S::kBlock == kBlock) {
-      if (tuning_variant() == 152 && al16 && stride % 16 == 0) {  // at most 128 VGPRs: 4 waves per SIMD
-        g_kernel = "k_global<fixed,a16,lines,wpe4>@8";
-        k_global<false, Algo, SinkNt, true, kLongLines, S::kBlock, 4><<<g, S::kBlock, 0, st>>>(
-            k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-        HIP_TRY(hipGetLastError());
-        return 0;
-      }
-    }
-#endif
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 155 && al16 && stride % 16 == 0) {  // CRC chunks streamed line by line
-      g_kernel = S::kBlock == kBlock ? "k_global<fixed,a16,stream>@8" : "k_global<fixed,a16,stream,crc8,768>@1";
-      k_global<false, Algo, SinkNt, true, kLongStream, S::kBlock><<<g, S::kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-#endif
+    // window): per-lane global reads, the 6-bit tables in LDS, 8 WG/CU
+    // (VGPR-bound to 3 waves per SIMD)
+    const unsigned g = grid_for(blocks, 8, dev);
     if (al16 && stride % 16 == 0) {
-      g_kernel = S::kBlock == kBlock ? "k_global<fixed,a16,lines>@8" : "k_global<fixed,a16,lines,crc8,768>@1";
-      k_global<false, Algo, SinkNt, true, kLongLines, S::kBlock><<<g, S::kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+      g_kernel = "k_global<fixed,a16,lines>@8";
+      k_global<false, Algo, SinkNt, true, kLongLines><<<g, kBlock, 0, st>>>(k, nullptr, 0, stride, keylen, n,
+                                                                             algo, sink_nt);
     } else {
-      g_kernel = S::kBlock == kBlock ? "k_global<fixed>@8" : "k_global<fixed,crc8,768>@1";
-      k_global<false, Algo, SinkNt, false, 0, S::kBlock><<<g, S::kBlock, 0, st>>>(k, nullptr, 0, stride,
-                                                                                  keylen, n, algo, sink_nt);
+      g_kernel = "k_global<fixed>@8";
+      k_global<false, Algo, SinkNt><<<g, kBlock, 0, st>>>(k, nullptr, 0, stride, keylen, n, algo, sink_nt);
     }
   } else {
     const u64 tiles = (n + 63) / 64;
@@ -324,18 +302,6 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
 #ifdef PDHT_HIP_TUNING
   if (tuning_variant() == 12) wide = false;
   if (tuning_variant() == 13) wide = true;
-  if (tuning_variant() == 156 || tuning_variant() == 157) {  // no LDS window: per-lane reads from global memory
-    const bool w4 = tuning_variant() == 156;
-    g_kernel = w4 ? "k_global<var,wide>@8" : "k_global<var>@8";
-    if (w4)
-      k_global<true, Algo, SinkNt, false, kVarWide><<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, st>>>(
-          b, offsets, obase, 0, 0, n, algo, sink_nt);
-    else
-      k_global<true, Algo, SinkNt><<<grid_for((n + kBlock - 1) / kBlock, 8, dev), kBlock, 0, st>>>(
-          b, offsets, obase, 0, 0, n, algo, sink_nt);
-    HIP_TRY(hipGetLastError());
-    return 0;
-  }
 #endif
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";

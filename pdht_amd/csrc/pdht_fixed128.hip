@@ -22,10 +22,6 @@ PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t k
   if (n && !out) return fail("null out%s", "");
   if (keylen > 900) {  // CityHashCrc256 rounds: CRC-32C tables in LDS
 #ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 151)  // r03 byte tables with v_perm addresses (768-thread workgroups)
-      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 8>{}, Sink128{nullptr, out}, ST(s));
-    if (tuning_variant() == 154)  // plain byte tables, SDWA addresses, 8 WG/CU
-      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 7>{}, Sink128{nullptr, out}, ST(s));
     if (tuning_variant() == 153)  // timing only: no CRC lookups (wrong digests)
       return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 0>{}, Sink128{nullptr, out}, ST(s));
 #endif

@@ -19,14 +19,8 @@ extern "C" {
  *              80/81  1024-thread transpose at 1 / 2 WG/CU (cfg1 shape)
  *                 82  the 256-thread transpose whatever the histogram
  *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
- *                151  CRC-32C byte tables, v_perm addresses, 768-thread workgroups
- *                152  the 6-bit form held to 128 VGPRs (4 waves per SIMD; spills)
  *                153  timing only: CRC lookups replaced by a fold (wrong digests)
- *                154  plain slicing-by-8 tables (8 KiB), one SDWA shift per lookup address
- *                155  CRC-256 chunks streamed line by line (one 128-B line in flight per lane)
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
- *            156 / 157 no window: per-lane reads from global memory (16-B loads at
- *                     4-B alignment / dword loads), 8 WG/CU
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,
  *                     41 default-policy DMA, 42 plain stores, 43 3 WG/CU,
@@ -38,9 +32,7 @@ extern "C" {
  *                     into 32 KiB (L2-resident)
  *   cfg3 path 140-144 (pdht_city64_batch_var_dev) digests wrapped into 32 KiB
  *                     / 2 / 8 / 32 / 128 MiB of out (wrong digests: where the
- *                     writes land); 145-147 two-phase: 4M / 1M / 4M-key chunks
- *                     hashed into a scratch buffer (nt / nt / plain stores),
- *                     then copied to out
+ *                     writes land)
  *   launches  114-118 key bytes per launch: 256 MiB / 1 GiB / 2 GiB / 4 GiB /
  *                     all in one launch (product: 512 MiB)
  *   bucketing     21  generic-length scatter for 8/16/32-B keys

@@ -8,13 +8,11 @@ PDHT_API int pdht_city64_batch_var_dev(const void *bytes, size_t nbytes, const u
                                        size_t n, uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
 #ifdef PDHT_HIP_TUNING
-  // r03 write-destination experiments on the product window kernel:
-  // 140-144 nt digest stores wrapped into 32 KiB / 2 / 8 / 32 / 128 MiB of
-  // out (calibration: wrong digests); 145-147 two-phase: chunks of 4M / 1M /
-  // 4M keys hashed into a scratch buffer (145/146 nt stores, 147 plain),
-  // each chunk's digests then copied to out (device-to-device)
+  // r03 write-destination calibration of the product window kernel: 140-144
+  // nt digest stores wrapped into 32 KiB / 2 / 8 / 32 / 128 MiB of out
+  // (wrong digests: what the HBM writes cost)
   const int v = tuning_variant();
-  if (v >= 140 && v <= 147 && n) {
+  if (v >= 140 && v <= 144 && n) {
     int dev;
     if (int rc = current_device(&dev)) return rc;
     const uint8_t *b = static_cast<const uint8_t *>(bytes);
@@ -25,27 +23,12 @@ PDHT_API int pdht_city64_batch_var_dev(const void *bytes, size_t nbytes, const u
           b, offsets + k0, 0, 0, 0, c, AlgoCity64{}, sink);
     };
     g_kernel = "k_window<var,nt,10224>@4";
-    if (v <= 144) {
-      if (v == 140) win(0, n, SinkRing<12>{nullptr, out});
-      if (v == 141) win(0, n, SinkRing<18>{nullptr, out});
-      if (v == 142) win(0, n, SinkRing<20>{nullptr, out});
-      if (v == 143) win(0, n, SinkRing<22>{nullptr, out});
-      if (v == 144) win(0, n, SinkRing<24>{nullptr, out});
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-    static u64 *scratch = nullptr;
-    const u64 C = v == 146 ? (1ull << 20) : (4ull << 20);
-    if (!scratch) HIP_TRY(hipMalloc(&scratch, (4ull << 20) * 8));
-    for (u64 k0 = 0; k0 < n; k0 += C) {
-      const u64 c = std::min<u64>(C, n - k0);
-      if (v == 147)
-        win(k0, c, Sink64{nullptr, scratch});
-      else
-        win(k0, c, Sink64T<true>{nullptr, scratch});
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(out + k0, scratch, c * 8, hipMemcpyDeviceToDevice, st));
-    }
+    if (v == 140) win(0, n, SinkRing<12>{nullptr, out});
+    if (v == 141) win(0, n, SinkRing<18>{nullptr, out});
+    if (v == 142) win(0, n, SinkRing<20>{nullptr, out});
+    if (v == 143) win(0, n, SinkRing<22>{nullptr, out});
+    if (v == 144) win(0, n, SinkRing<24>{nullptr, out});
+    HIP_TRY(hipGetLastError());
     return 0;
   }
 #endif
