@@ -179,11 +179,12 @@ template <class Out>
 static StagedShape staged_shape(size_t keysize, u32 nranks) {
   if (nranks < 512) return StagedShape::kBallot4x16;
   if (!std::is_same<Out, OutSoA>::value) {
-    // records: owner ranking pays for 16/32-B keys only (ab_records_*_shapes.log:
-    // 16-B at 1024 ranks 0.62 -> 0.56 ms, 32-B 1.29 -> 1.20); 8-B records
-    // lose 3 % with it
-    if (keysize != 8 && staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024)
-      return StagedShape::kOwner4x16;
+    // records: owner ranking on 4 x 16 tiles (ab_records_*_shapes.log: 16-B
+    // at 1024 ranks 0.62 -> 0.56 ms, 32-B 1.29 -> 1.20); 8-B records lost 3 %
+    // with it in r02, and gain 6 % since both halves of a record leave
+    // together (r03, profiles/r03/ab/records_shapes.log: 1024 ranks 0.296 ->
+    // 0.277 ms, 512 ranks 0.273 -> 0.258); 8 x 16 tiles lose for every size
+    if (staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024) return StagedShape::kOwner4x16;
     return StagedShape::kBallot4x16;
   }
   if (keysize != 32 && staged_lds_bytes(nranks, 8, 16, false, 2) <= 160 * 1024) return StagedShape::kOwner8x16;
