@@ -256,3 +256,20 @@ def test_batch_fails_loudly_without_gpu():
     t = P.PdhtTable(keysize=8)
     with pytest.raises(P.PdhtError):
         t.hash_batch(np.zeros((4, 8), dtype=np.uint8))
+
+
+def test_every_tuning_variant_is_documented():
+    """Every variant number the sources select on is listed in
+    pdht_hip_tuning.h (the list had gone stale)."""
+    import glob
+    import re
+    src = "".join(open(p).read() for p in glob.glob(os.path.join(ROOT, "pdht_amd", "csrc", "*.h*"))
+                  if not p.endswith("pdht_hip_tuning.h"))
+    used = {int(x) for x in re.findall(r"tuning_variant\(\) == (\d+)", src)}
+    used |= {int(x) for x in re.findall(r"\bv == (\d+)", src)}
+    for lo, hi in re.findall(r"v >= (\d+) && v <= (\d+)", src):
+        used |= set(range(int(lo), int(hi) + 1))
+    doc = open(os.path.join(ROOT, "pdht_amd", "csrc", "pdht_hip_tuning.h")).read()
+    listed = {int(x) for x in re.findall(r"\b(\d+)\b", doc)}
+    listed |= {n for lo, hi in re.findall(r"\b(\d+)-(\d+)\b", doc) for n in range(int(lo), int(hi) + 1)}
+    assert used and not (used - listed), sorted(used - listed)
