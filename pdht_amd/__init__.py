@@ -297,27 +297,42 @@ def _torch():
 
 
 class _on:
-    """Device guard + stream of one device-side call."""
+    """Device guard + stream of one device-side call.  The device switch and
+    the current-stream lookup go through torch's raw accessors when they
+    exist (a batch call's host cost is what a 1M-key batch waits for:
+    tools/call_overhead.py)."""
+
+    __slots__ = ("device", "index", "stream_obj", "prev", "stream")
 
     def __init__(self, device, stream=None):
-        torch = _torch()
         if device.type != "cuda":
             raise ValueError("expected CUDA tensors")
         self.device = device
-        self.guard = torch.cuda.device(device)
+        self.index = device.index if device.index is not None else _torch().cuda.current_device()
         self.stream_obj = stream
         if stream is not None and stream.device != device:
             raise ValueError(f"stream is on {stream.device}, tensors on {device}")
 
     def __enter__(self):
-        torch = _torch()
-        self.guard.__enter__()
-        s = self.stream_obj if self.stream_obj is not None else torch.cuda.current_stream(self.device)
-        self.stream = C.c_void_p(s.cuda_stream)
+        tc = _torch()._C
+        if hasattr(tc, "_cuda_getDevice") and hasattr(tc, "_cuda_getCurrentRawStream"):
+            self.prev = tc._cuda_getDevice()
+            if self.prev != self.index:
+                tc._cuda_setDevice(self.index)
+            s = self.stream_obj.cuda_stream if self.stream_obj is not None else \
+                tc._cuda_getCurrentRawStream(self.index)
+        else:
+            torch = _torch()
+            self.prev = torch.cuda.current_device()
+            torch.cuda.set_device(self.index)
+            s = (self.stream_obj if self.stream_obj is not None else torch.cuda.current_stream(self.device)).cuda_stream
+        self.stream = C.c_void_p(s)
         return self
 
     def __exit__(self, *exc):
-        return self.guard.__exit__(*exc)
+        if self.prev != self.index:
+            _torch().cuda.set_device(self.prev)
+        return False
 
 
 def _dptr(t) -> C.c_void_p:
