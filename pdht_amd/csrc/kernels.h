@@ -215,6 +215,19 @@ struct CrcNullTab {
   const u32 *t;
   __device__ __forceinline__ u32 crc64(u64 x) const { return (u32)x ^ (u32)(x >> 32) ^ t[0]; }
 };
+// Plain slicing-by-8 byte tables (8 KiB, one copy), each address one SDWA
+// byte select: 8 lookups of ~2 VOP2 per word against the 6-bit form's 11 of
+// ~3 (r03: equal in short A/B runs; re-timed for sustained runs, where the
+// VALU-dense loop holds a lower clock).
+struct CrcLdsByteTab {
+  const u32 *t;  // [8][256], table k for byte k of the word (= slice-8 table 7-k)
+  __device__ __forceinline__ u32 rd(u32 k, u32 b) const { return t[256 * k + b]; }
+  __device__ __forceinline__ u32 crc64(u64 x) const {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    return rd(0, lo & 255) ^ rd(1, (lo >> 8) & 255) ^ rd(2, (lo >> 16) & 255) ^ rd(3, lo >> 24) ^
+           rd(4, hi & 255) ^ rd(5, (hi >> 8) & 255) ^ rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24);
+  }
+};
 #endif
 
 template <int SB>
@@ -235,6 +248,15 @@ struct CrcLdsSlices<0> {  // CrcNullTab: the 6-bit form's launch shape, no looku
   static constexpr u32 kWords = 64;
   __device__ static void fill(u32 *tab) {
     for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = 0;
+  }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
+};
+template <>
+struct CrcLdsSlices<8> {  // CrcLdsByteTab
+  typedef CrcLdsByteTab Tab;
+  static constexpr u32 kWords = 8 * 256;
+  __device__ static void fill(u32 *tab) {
+    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrcDev.t[7 - (k >> 8)][k & 255];
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };

@@ -24,6 +24,8 @@ PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t k
 #ifdef PDHT_HIP_TUNING
     if (tuning_variant() == 153)  // timing only: no CRC lookups (wrong digests)
       return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 0>{}, Sink128{nullptr, out}, ST(s));
+    if (tuning_variant() == 154)  // slicing-by-8 byte tables in LDS
+      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 8>{}, Sink128{nullptr, out}, ST(s));
 #endif
     return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 6>{}, Sink128{nullptr, out}, ST(s));
   }

@@ -133,6 +133,17 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
         [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:300]]
 
 
+@pytest.mark.tuning
+@pytest.mark.parametrize("L", [901, 1024, 2200])
+def test_crc128_long_keys_byte_tables(dev, oracle, L):
+    """Tuning variant 154: the long-key CRC-32C on slicing-by-8 byte tables."""
+    rng = np.random.default_rng(L + 5)
+    k = rng.integers(0, 256, (20_001, L), dtype=np.uint8)
+    with P.tuning(154):
+        got = u64(P.citycrc128_batch(to_dev(k, dev)))
+    assert (got == oracle.city128_fixed(k, crc=True)).all()
+
+
 @pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 256, 300, 384, 400, 1200])
 def test_seeded_batches(dev, oracle, L):
     rng = np.random.default_rng(77 + L)
