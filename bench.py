@@ -332,19 +332,23 @@ def main():
         step()
     kernel_name = P.last_kernel()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
+    # One event pair around the K steps, on the stream the kernels are launched
+    # on: the launches queue back to back as a pipelined caller's would.
+    # (r01-r03 bracketed every step with its own pair; on a 15-us launch
+    # (cfg1) the two records per step outlasted the kernel, so the GPU idled
+    # between steps waiting for the host and the per-step pairs timed that.)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:  # events on the stream the kernels are launched on
-        s.record()
+    ev0.record()
+    for _ in range(a.steps):
         step()
-        e.record()
+    ev1.record()
     torch.cuda.synchronize()
     D.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
     elapsed_max, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=dev)
 
     # -------------------------------------------- achievable read stream ---

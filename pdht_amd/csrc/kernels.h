@@ -189,13 +189,14 @@ struct AlgoCrc128Seed {
 };
 
 // CRC-32C tables in LDS for batches that may hold keys > 900 B
-// (CityHashCrc256 path, city.c:407-517): the 6-bit-slice tables of
-// city_core.h (Crc32c6Tables), 11 x 64 entries = 2816 B per workgroup, every
-// lookup conflict-free.  (r01 kept the slicing-by-8 tables here, 8 KiB: one
-// lookup per byte but 4.3x bank conflicts; r02's 5-bit slices, 13 lookups per
-// word, measured 2 % slower; from constant memory the lookups are per-lane
-// vector loads through the TA, 4x slower again.)
-// The 6-bit-slice form (city_core.h Crc32c6Tables): 11 lookups per word.
+// (CityHashCrc256 path, city.c:407-517).  Two forms: the slicing-by-8 byte
+// tables (CrcLdsByteTab below, 8 KiB per workgroup, the product again from
+// r03) and the 6-bit-slice tables of city_core.h (Crc32c6Tables), 11 x 64
+// entries = 2816 B, every lookup conflict-free but 11 lookups per word (r02's
+// product; r01's byte tables lost to them on r01's long-key kernel, r03's
+// line-span kernel spends more on VALU than on bank conflicts).  r02's 5-bit
+// slices, 13 lookups per word, measured 2 % slower than 6-bit; from constant
+// memory the lookups are per-lane vector loads through the TA, 4x slower.
 struct CrcLds6Tab {
   const u32 *t;  // [11][64]
   __device__ __forceinline__ u32 crc64(u64 x) const {
@@ -208,17 +209,11 @@ struct CrcLds6Tab {
     return r;
   }
 };
-#ifdef PDHT_HIP_TUNING
-// Timing only: the CRC-32C of a word replaced by a fold (no table lookups):
-// what the lookups cost the long-key kernel (wrong digests).
-struct CrcNullTab {
-  const u32 *t;
-  __device__ __forceinline__ u32 crc64(u64 x) const { return (u32)x ^ (u32)(x >> 32) ^ t[0]; }
-};
-// Plain slicing-by-8 byte tables (8 KiB, one copy), each address one SDWA
-// byte select: 8 lookups of ~2 VOP2 per word against the 6-bit form's 11 of
-// ~3 (r03: equal in short A/B runs; re-timed for sustained runs, where the
-// VALU-dense loop holds a lower clock).
+// The product form (r03): plain slicing-by-8 byte tables (8 KiB, one copy),
+// each address one byte select: 8 lookups of ~2 VALU per word against the
+// 6-bit form's 11 of ~3.  Byte-indexed tables conflict in LDS (+72 % bank
+// conflicts), but the long-key loop is VALU-heavy and the byte tables run
+// 3-4 % faster (interleaved, `profiles/r03/ab/long_bytetab_*.log`).
 struct CrcLdsByteTab {
   const u32 *t;  // [8][256], table k for byte k of the word (= slice-8 table 7-k)
   __device__ __forceinline__ u32 rd(u32 k, u32 b) const { return t[256 * k + b]; }
@@ -227,6 +222,13 @@ struct CrcLdsByteTab {
     return rd(0, lo & 255) ^ rd(1, (lo >> 8) & 255) ^ rd(2, (lo >> 16) & 255) ^ rd(3, lo >> 24) ^
            rd(4, hi & 255) ^ rd(5, (hi >> 8) & 255) ^ rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24);
   }
+};
+#ifdef PDHT_HIP_TUNING
+// Timing only: the CRC-32C of a word replaced by a fold (no table lookups):
+// what the lookups cost the long-key kernel (wrong digests).
+struct CrcNullTab {
+  const u32 *t;
+  __device__ __forceinline__ u32 crc64(u64 x) const { return (u32)x ^ (u32)(x >> 32) ^ t[0]; }
 };
 #endif
 
@@ -251,8 +253,9 @@ struct CrcLdsSlices<0> {  // CrcNullTab: the 6-bit form's launch shape, no looku
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };
+#endif
 template <>
-struct CrcLdsSlices<8> {  // CrcLdsByteTab
+struct CrcLdsSlices<8> {  // CrcLdsByteTab: the product tables
   typedef CrcLdsByteTab Tab;
   static constexpr u32 kWords = 8 * 256;
   __device__ static void fill(u32 *tab) {
@@ -260,8 +263,8 @@ struct CrcLdsSlices<8> {  // CrcLdsByteTab
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };
-#endif
-template <class Base, int SB = 6>
+constexpr int kCrcSlices = 8;  // the product's CRC-32C tables (tuning variant 150: 6)
+template <class Base, int SB = kCrcSlices>
 struct CrcLds : Base {
   static constexpr bool kCrcLds = true;
   typedef CrcLdsSlices<SB> Slices;

@@ -20,14 +20,14 @@ PDHT_API int pdht_city128_seed_batch_dev(const void *keys, size_t stride, size_t
 PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t keylen, size_t n,
                                        uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
-  if (keylen > 900) {  // CityHashCrc256 rounds: CRC-32C tables in LDS
+  if (keylen > 900) {  // CityHashCrc256 rounds: CRC-32C byte tables in LDS
 #ifdef PDHT_HIP_TUNING
     if (tuning_variant() == 153)  // timing only: no CRC lookups (wrong digests)
       return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 0>{}, Sink128{nullptr, out}, ST(s));
-    if (tuning_variant() == 154)  // slicing-by-8 byte tables in LDS
-      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 8>{}, Sink128{nullptr, out}, ST(s));
+    if (tuning_variant() == 150)  // r02's 6-bit-slice tables
+      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 6>{}, Sink128{nullptr, out}, ST(s));
 #endif
-    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 6>{}, Sink128{nullptr, out}, ST(s));
+    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
   }
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));
 }
@@ -37,7 +37,7 @@ PDHT_API int pdht_citycrc128_seed_batch_dev(const void *keys, size_t stride, siz
                                             pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
   if (keylen > 900)
-    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128Seed, 6>{{lo, hi}}, Sink128{nullptr, out},
+    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128Seed>{{lo, hi}}, Sink128{nullptr, out},
                         ST(s));
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128Seed{lo, hi}, Sink128{nullptr, out}, ST(s));
 }

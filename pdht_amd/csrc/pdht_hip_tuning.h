@@ -20,7 +20,7 @@ extern "C" {
  *                 82  the 256-thread transpose whatever the histogram
  *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
  *                153  timing only: CRC lookups replaced by a fold (wrong digests)
- *                154  CRC-32C on slicing-by-8 byte tables in LDS (8 KiB)
+ *                150  CRC-32C on r02's 6-bit-slice tables (product: byte tables)
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,

@@ -229,7 +229,7 @@ PDHT_API int pdht_citycrc128_batch_host(const void *keys, size_t keylen, size_t 
   return host_fixed(keys, keylen, n, 16, out, device,
                     [&](const uint8_t *dk, size_t cnt, uint8_t *dout, hipStream_t st) {
                       if (keylen > 900)
-                        return launch_fixed(dk, keylen, keylen, cnt, CrcLds<AlgoCrc128, 6>{},
+                        return launch_fixed(dk, keylen, keylen, cnt, CrcLds<AlgoCrc128>{},
                                             Sink128{nullptr, reinterpret_cast<u64 *>(dout)}, st);
                       return launch_fixed(dk, keylen, keylen, cnt, AlgoCrc128{},
                                           Sink128{nullptr, reinterpret_cast<u64 *>(dout)}, st);

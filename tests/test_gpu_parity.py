@@ -135,11 +135,11 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
 
 @pytest.mark.tuning
 @pytest.mark.parametrize("L", [901, 1024, 2200])
-def test_crc128_long_keys_byte_tables(dev, oracle, L):
-    """Tuning variant 154: the long-key CRC-32C on slicing-by-8 byte tables."""
+def test_crc128_long_keys_6bit_tables(dev, oracle, L):
+    """Tuning variant 150: the long-key CRC-32C on r02's 6-bit-slice tables."""
     rng = np.random.default_rng(L + 5)
     k = rng.integers(0, 256, (20_001, L), dtype=np.uint8)
-    with P.tuning(154):
+    with P.tuning(150):
         got = u64(P.citycrc128_batch(to_dev(k, dev)))
     assert (got == oracle.city128_fixed(k, crc=True)).all()
 

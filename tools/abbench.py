@@ -176,6 +176,7 @@ def main():
         med = float(np.median(t["ms"]))
         rows.append({"work": a.work, "variant": v, "per_cu": pc, "kernel": t["kernel"], "ok": t["ok"],
                      "median_ms": round(med, 4), "min_ms": round(float(np.min(t["ms"])), 4),
+                     "mean_ms": round(float(np.mean(t["ms"])), 4), "max_ms": round(float(np.max(t["ms"])), 4),
                      "GBps": round(nbytes / med / 1e6, 1), "frac_8TBps": round(nbytes / med / 1e6 / 8000, 4)})
     for r in sorted(rows, key=lambda r: r["median_ms"]):
         print(json.dumps(r), flush=True)
