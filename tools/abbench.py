@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--per-cu", default="0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--pair", action="store_true",
+                    help="one event pair around each round's reps (launches queue back to back, as "
+                         "bench.py times them); default: a pair per launch")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     step, result, nbytes = workload(a.work, dev)
@@ -163,6 +166,15 @@ def main():
     for _ in range(a.rounds):
         for v, pc in combos:
             with Ctx(v, pc):
+                if a.pair:
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    for _ in range(a.reps):
+                        step()
+                    e.record()
+                    torch.cuda.synchronize()
+                    stats[(v, pc)]["ms"].append(s.elapsed_time(e) / a.reps)
+                    continue
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(a.reps)]
                 for s, e in ev:

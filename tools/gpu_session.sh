@@ -3,8 +3,8 @@
 # first step that crashes (rc > 1) so nothing else touches a faulted GPU.
 #   tools/gpu_session.sh tests smoke bench bench_cfg3 ab_cfg2 prof_cfg2 pmc_cfg2 sq_long
 # Knobs (environment of the session script only, never read by the library):
-#   K=<pytest -k expr> for ktests; VARIANTS / PERCU / ROUNDS / REPS / TAG (log
-#   name suffix) for ab_*; PMCS for pmc_*.
+#   K=<pytest -k expr> for ktests; VARIANTS / PERCU / ROUNDS / REPS / PAIR=1 /
+#   TAG (log name suffix) for ab_*; PMCS for pmc_*.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -33,7 +33,7 @@ for step in "$@"; do
              timeout -k 10 300 python bench.py --config $cfg > "gpurun_out/$step.log" 2>&1; rc=$?
              tail -1 "gpurun_out/$step.log" | cut -c1-600 ;;
     ab_*)    w=${step#ab_}
-             timeout -k 10 400 python tools/abbench.py --work $w --variants ${VARIANTS:-0} --per-cu ${PERCU:-0} --rounds ${ROUNDS:-5} --reps ${REPS:-10} > "gpurun_out/$step${TAG:-}.log" 2>&1; rc=$?
+             timeout -k 10 400 python tools/abbench.py --work $w --variants ${VARIANTS:-0} --per-cu ${PERCU:-0} --rounds ${ROUNDS:-5} --reps ${REPS:-10} ${PAIR:+--pair} > "gpurun_out/$step${TAG:-}.log" 2>&1; rc=$?
              grep -v amdgpu.ids "gpurun_out/$step${TAG:-}.log" | cut -c1-260 ;;
     prof_*)  cfg=${step#prof_}; d="gpurun_out/$step"
              timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$d" -o run --output-format csv -- python3 bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline --no-host > "$d.log" 2>&1; rc=$?
