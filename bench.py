@@ -17,8 +17,9 @@ timing barrier, the max of elapsed times and the parity reductions.
 
 Rank 0 prints one JSON line.  Besides the contract fields it carries
   roofline      -- achieved algorithmic HBM GB/s of the hash kernel (72 B/key:
-                   64 B key read + 8 B digest write) over its average launch
-                   duration measured with HIP events on the launch stream,
+                   64 B key read + 8 B digest write) over its average step
+                   time: one pair of HIP events on the launch stream around
+                   the K timed steps (launches queued back to back),
                    plus HBM traffic per launch from the committed rocprofv3
                    PMC pass (profiles/traffic_<cfg>.json), a calibrated
                    read-stream rate on the same buffer and (64-B configs) the
@@ -248,9 +249,11 @@ def main():
         words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
         hist = torch.zeros(4, dtype=torch.int64, device=dev)
-        outs = P.place_batch(keys, 1, 4, hist=hist)
+        # a 15-us launch: the step is the C call a C caller makes per batch
+        # (pdht_place_batch_dev, checks and pointer lookups bound once), so
+        # that the Python mirror's per-call cost does not set the step time
+        step, outs = P.bind_place_batch(keys, 1, 4, hist=hist)
         out = outs[0]
-        step = lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)  # noqa: E731
         bytes_per_key = 64 + 8 + 4 + 4
         workload = f"cfg1: pdht_hash placement (mbits+ptindex+rank+hist) of {n >> 20}M x 64B keys per GPU"
         total_bytes_in = n * L

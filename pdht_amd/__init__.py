@@ -525,6 +525,42 @@ def place_batch(keys, nptes: int, nranks: int, *, ptindex=True, rank=True, hist=
     return mb, pt, rk
 
 
+def bind_place_batch(keys, nptes: int, nranks: int, *, hist=None, stream=None, out=None):
+    """place_batch prepared once for repeated calls on the same tensors.
+
+    The checks, pointer and stream lookups run here; the returned callable
+    makes only the C call (pdht_place_batch_dev on the stream current now),
+    i.e. a C caller's per-batch cost.  Returns (call, (mbits, ptindex, rank)).
+    The caller keeps keys.device current and the tensors alive.
+    """
+    torch = _torch()
+    n, L, stride = _keys_2d(keys)
+    if stride != L:
+        raise ValueError("bind_place_batch needs packed keys")
+    dev = keys.device
+    if hist is not None:
+        _need(hist, "hist", torch.int64, dev, numel=nranks)
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+               torch.empty(n, dtype=torch.int32, device=dev))
+    mb, pt, rk = out
+    _need(mb, "out[0] (mbits)", torch.int64, dev, shape=(n,))
+    _need(pt, "out[1] (ptindex)", torch.int32, dev, shape=(n,))
+    _need(rk, "out[2] (rank)", torch.int32, dev, shape=(n,))
+    f = lib().pdht_place_batch_dev
+    with _on(dev, stream) as g:
+        st = g.stream
+    vals = (_dptr(keys), L, n, nptes, nranks, _dptr(mb), _dptr(pt), _dptr(rk), 4, _opt(hist), st)
+    args = tuple(a if isinstance(a, C._SimpleCData) or a is None else t(a) for t, a in zip(f.argtypes, vals))
+
+    def call():
+        rc = f(*args)
+        if rc:
+            _check(rc, "pdht_place_batch_dev")
+
+    return call, out
+
+
 def bucket_workspace_bytes(n: int, keysize: int, nranks: int) -> int:
     return lib().pdht_bucket_workspace_bytes(n, keysize, nranks)
 

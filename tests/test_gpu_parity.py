@@ -410,6 +410,23 @@ def test_place_hist_64B_large_batch(dev, oracle):
     assert (u64(mb) % 4 == r_all).all() and (pt.cpu().numpy() == 0).all()
 
 
+@pytest.mark.parametrize("L", [8, 64])
+def test_bind_place_batch(dev, oracle, L):
+    """The prepared call (bench.py cfg1's step): same digests, ptindex and
+    ranks as place_batch, and the histogram accumulates over repeated calls."""
+    rng = np.random.default_rng(L + 17)
+    k = rng.integers(0, 256, (70_001, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    hist = torch.zeros(1000, dtype=torch.int64, device=dev)
+    call, (mb, pt, rk) = P.bind_place_batch(kd, 3, 1000, hist=hist)
+    call()
+    call()
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, 1000)
+    assert (u64(mb) == m2).all()
+    assert (pt.cpu().numpy().view(np.uint32) == p2).all() and (rk.cpu().numpy().view(np.uint32) == r2).all()
+    assert (hist.cpu().numpy() == 2 * np.bincount(r2, minlength=1000)).all()
+
+
 @pytest.mark.parametrize("L", [8, 16, 32])
 def test_small_keys(dev, oracle, L):
     rng = np.random.default_rng(L)
