@@ -261,7 +261,20 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   const size_t hist_lds = (size_t)nranks * 4;
   TwoPass tp{};
   if (kind == BucketKernel::kTwoPass) {
+    // rank = c * F + f.  Array outputs of 8/16-B keys take one fine bit more
+    // than the balanced split (8192 ranks: F = 256, C = 32): pass 2 writes
+    // 24 / 32 B per key in runs of ~4096 / C keys against pass 1's 12 / 20 B
+    // in runs of ~4096 / F, so longer pass-2 runs pay.  Three boxes, 16M keys
+    // (profiles/r03/ab/bucket_two_pass_digits.log): 8 B at 8192 ranks -5.5 /
+    // 0 / -3.6 %, 16 B at 4096 ranks -4.3 / -4.0 %, 2048 ranks within +-2 %.
+    // 32-B keys (pass 1 writes 36 B/key) lose 3 % with it, and records (AoS
+    // rows, pass-2 runs already >= 1 KiB) 1 %: both keep the balanced split.
     tp.fbits = (a.nbits + 1) / 2;
+    bool fine_plus = std::is_same<Out, OutSoA>::value && keysize <= 16;
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 164) fine_plus = false;  // the balanced split (r02-r03)
+#endif
+    if (fine_plus && tp.fbits + 1 <= std::min<u32>(8, a.nbits)) ++tp.fbits;
     tp.F = 1u << tp.fbits;
     tp.C = (nranks + tp.F - 1) >> tp.fbits;
     tp.cbits = a.nbits - tp.fbits;

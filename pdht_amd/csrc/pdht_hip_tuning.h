@@ -41,6 +41,8 @@ extern "C" {
  *                 71  two passes from 2 ranks up
  *              83/87  owner-table ranking on 8 x 16 / 4 x 16 tiles, any nranks
  *              85/89  ballot ranking, any nranks (85: static tile order)
+ *                164  two-pass arrays of 8/16-B keys on the balanced digit split
+ *                     F = 2^ceil(nbits/2) (product: one fine bit more)
  *   records      112  r02 store order (header halves a staging round early)
  *   host          61  chunked copy pipeline instead of zero-copy on pinned buffers
  * Process-wide; returns the previous value. */

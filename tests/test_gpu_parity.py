@@ -485,6 +485,11 @@ BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535
 BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
                  for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
+# 164: two-pass arrays on the balanced digit split (the product takes one fine bit more)
+BUCKET_CASES += [(L, nr, n, 164) for L in (8, 16, 32) for nr in (1025, 2049, 4097, 8192)
+                 for n in (4095, 300007, (1 << 20) + 5)]
+# the product's fine-plus split at its edges: 71 forces two passes from 2 ranks (nbits 1..3)
+BUCKET_CASES += [(L, nr, 70001, 71) for L in (8, 32) for nr in (2, 3, 4, 5, 8, 9)]
 
 
 def _bucket_kernel(L, nranks, variant, records=False):
@@ -597,9 +602,6 @@ RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n i
 RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]
 # 112: the r02 store order of 8-B records (header halves a staging round early)
 RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
-# records switch to owner-table ranking for 16/32-B keys from 512 ranks while
-# two workgroups fit a CU (staged_shape): both edges of both thresholds
-RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]
 
 
 @pytest.mark.parametrize("L,nranks,n,variant", _tuning_marked(RECORD_CASES))
