@@ -15,6 +15,12 @@ collective on the data path (weak scaling); the only collectives are the
 timing barrier, the max of elapsed times and the parity reductions.
 "cfg5" = 128M keys per GPU, i.e. BASELINE configs[4] (1B keys) at N = 8.
 
+The default run also times BASELINE configs[4] at its own N: the 1B x 64 B
+stream split contiguously over the N ranks (1B/N keys per GPU, strong
+scaling; "baseline_config4" block, parity from the committed 16M-key chunk
+folds).  `--dist-backend gloo` rehearses the N-rank path on fewer GPUs (ranks
+share devices; RCCL refuses two ranks on one GPU).
+
 Rank 0 prints one JSON line.  Besides the contract fields it carries
   roofline      -- achieved algorithmic HBM GB/s of the hash kernel (72 B/key:
                    64 B key read + 8 B digest write) over its average step
@@ -77,6 +83,11 @@ def parse():
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.5,
                     help="wall budget of one CPU-baseline pass (best of 5 passes)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend at N > 1: nccl (= RCCL, one GPU per rank) or gloo (a rehearsal: "
+                         "ranks share the visible GPUs round-robin, collectives on CPU tensors)")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="skip the BASELINE configs[4] block (1B x 64 B keys split over the N ranks)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check only: every rank joins a gloo group, touches no GPU and rank 0 "
                          "prints one JSON line with the world (tests/test_bench_launch.py)")
@@ -141,10 +152,28 @@ def dry_run(a) -> None:
         dist.all_gather_object(allr, mine)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world, "ranks": allr,
-                          "gpus_arg": a.gpus, "backend": dist.get_backend() if world > 1 else None}),
+                          "gpus_arg": a.gpus, "backend": dist.get_backend() if world > 1 else None,
+                          "plan": plan(a, world)}),
               flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+CONFIG4_KEYS = 1 << 30  # BASELINE configs[4]: 1B x 64 B keys over the node's GPUs
+
+
+def plan(a, world: int) -> dict:
+    """What this run measures, decided before any GPU work (printed by
+    --dry-run, so the CPU tests can check it): the per-GPU workload of
+    `value` and, for the default config, the BASELINE configs[4] block -- the
+    1B x 64 B stream split over the N ranks (strong scaling), timed beside
+    the cfg2 weak-scaling value at every N."""
+    p = {"config": a.config, "value_scaling": "weak", "world_size": world, "backend": a.dist_backend}
+    if a.config == "cfg2" and not a.no_config4 and not a.keys_per_gpu:
+        p["config4"] = {"keys_total": CONFIG4_KEYS, "key_bytes": 64, "split": "strong (contiguous, 1B/N per rank)",
+                        "keys_per_rank": [CONFIG4_KEYS * (r + 1) // world - CONFIG4_KEYS * r // world
+                                          for r in range(world)]}
+    return p
 
 
 def golden_folds():
@@ -174,12 +203,19 @@ def main():
     from pdht_amd import dist as D
 
     rank, local, world = D.env_rank_world()
-    if world > 1:
+    if world > 1 and a.dist_backend == "gloo":
+        # rehearsal of the N-rank path on fewer GPUs (e.g. 2 ranks on the one
+        # GPU of a gpurun box, where RCCL refuses two ranks per device): ranks
+        # share devices round-robin, the collectives run on CPU tensors
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    cdev = dev if world > 1 and a.dist_backend == "nccl" else None  # where the collectives' tensors live
 
     if not os.path.exists(os.path.join(ROOT, "pdht_amd", "lib", "libpdht_hip.so")):
         import __graft_entry__
@@ -352,7 +388,7 @@ def main():
     D.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / a.steps
-    elapsed_max, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=dev)
+    elapsed_max, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=cdev)
 
     # -------------------------------------------- achievable read stream ---
     calib = None
@@ -398,20 +434,20 @@ def main():
 
     # ------------------------------------------------------------ parity ---
     if bucketed is not None and bucketed.get("records"):
-        parity = check_records(P, torch, D, sh, keys, bucketed, dev)
+        parity = check_records(P, torch, D, sh, keys, bucketed, dev, cdev)
     elif bucketed is not None:
-        parity = check_buckets(P, torch, D, sh, keys, bucketed, dev)
+        parity = check_buckets(P, torch, D, sh, keys, bucketed, dev, cdev)
     else:
         extra = None
         if cfg in ("place", "cfg1"):  # one fresh call: the timed ones accumulated into hist
             hist.zero_()
             extra = (*P.place_batch(keys, *((1, 4) if cfg == "cfg1" else (3, 1024)), hist=hist), hist)
         if cfg == "cfg2r":
-            ps = [check_parity(P, torch, D, "cfg2", sh, r, None, dev) for r in rot]
-            parity = ps[0] if all(p.startswith("ok") for p in ps) else "FAILED: " + " | ".join(ps)
-            parity += f" (all {len(rot)} rotating digest buffers)"
+            ps = [check_parity(P, torch, D, "cfg2", sh, r, None, cdev) for r in rot]
+            worst = min(ps, key=lambda p: list(PAR_WORD.values()).index(p.split(":")[0]))
+            parity = worst + f" (all {len(rot)} rotating digest buffers)"
         else:
-            parity = check_parity(P, torch, D, cfg, sh, out, extra, dev)
+            parity = check_parity(P, torch, D, cfg, sh, out, extra, cdev)
 
     # ------------------------------------------------------- report ------
     value = n * world * a.steps / elapsed_max / 1e9
@@ -436,8 +472,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
                      "traffic": load_traffic(cfg, n, kernel_name), "kernel": kernel_name,
-                     "kernel_ms": round(kern_ms, 4),
-                     "kernel_ms_max_rank": round(kern_ms_max, 4),
+                     "event_ms_per_step": round(kern_ms, 4),
+                     "event_ms_per_step_max_rank": round(kern_ms_max, 4),
+                     "timing": "one HIP-event pair on the launch stream around the K back-to-back steps, / K "
+                               "(includes any gap between launches; rocprofv3 kernel averages in profiles/)",
                      "read_only_GBps": round(total_bytes_in / (kern_ms / 1e3) / 1e9, 1),
                      "calibrated_read_stream_GBps": calib,
                      "calibrated_key_stream_GBps": calib_key},
@@ -447,15 +485,79 @@ def main():
         res["per_rank"] = D.per_rank_report(rank, local, world, n, bytes_per_key, kern_ms, elapsed, a.steps,
                                             PEAK_HBM_GBPS, device=dev)
     if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:  # (cfg2r: the same host path as cfg2)
-        hr = host_rate(P, torch, n, cfg, D, dev)
+        hr = host_rate(P, torch, n, cfg, D, dev, cdev)
         if rank == 0:
             res["host_resident"] = hr
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds, out, P, torch)
+    if "config4" in plan(a, world):
+        del keys, out, words
+        torch.cuda.empty_cache()
+        c4 = config4_block(P, torch, D, a, rank, local, world, dev, cdev)
+        if rank == 0:
+            res["baseline_config4"] = c4
+            w4 = c4["parity"].split(":")[0]
+            if w4 != "ok" and res["parity"].startswith("ok"):
+                res["parity"] = f"{w4}: " + res["parity"][4:] + " | configs[4] block: " + c4["parity"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def config4_block(P, torch, D, a, rank, local, world, dev, cdev) -> dict:
+    """BASELINE configs[4] at this world size: the 1B x 64 B key stream split
+    contiguously over the N ranks (strong scaling, pdht_amd.dist.strong_shard;
+    the reference places keys the same way, each SPMD rank hashing its own,
+    README.txt:20-22, libpdht/hash.c:29), keys generated in HBM, CityHash64
+    in ~512 MiB launches.  Timed as the main leg (barrier + synchronize on both
+    sides of K back-to-back steps, max over ranks) and checked bit-exact: each
+    rank's fold of its slice against the sum of the committed reference folds
+    of the 16M-key chunks it covers."""
+    sh = D.strong_shard(rank, world, CONFIG4_KEYS)
+    words = P.splitmix64_fill(SEED_KEYS, sh.first * 8, sh.n * 8, device=dev)
+    keys = words.view(torch.uint8).view(sh.n, 64)
+    out = torch.empty(sh.n, dtype=torch.int64, device=dev)
+    for _ in range(max(1, a.warmup // 5)):
+        P.city64_batch(keys, out=out)
+    steps = max(3, a.steps // 5)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    D.barrier()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        P.city64_batch(keys, out=out)
+    ev1.record()
+    torch.cuda.synchronize()
+    D.barrier()
+    elapsed = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1) / steps
+    elapsed_max = D.allreduce_max([elapsed], device=cdev)[0]
+    kernel = P.last_kernel()
+    want = city64_chunk_fold(golden_folds(), sh.first, sh.n)
+    if want is None:
+        st, msg = PAR_UNCHECKED, f"rank {rank}: no reference fold for keys {sh.first}..+{sh.n}"
+    else:
+        good = D.fold_tensor(out, sh.first) == want
+        st = PAR_OK if good else PAR_FAIL
+        msg = (f"rank {rank}: fold of keys {sh.first}..+{sh.n} {'==' if good else '!='} reference golden "
+               f"(16M-key chunks {sh.first >> 24}..{((sh.first + sh.n) >> 24) - 1})")
+    parity = combine_parity(D, st, [msg], world, cdev)
+    pr = D.per_rank_report(rank, local, world, sh.n, 72.0, ev_ms, elapsed,
+                           steps, PEAK_HBM_GBPS, device=dev)
+    value = CONFIG4_KEYS * steps / elapsed_max / 1e9
+    del keys, out, words
+    torch.cuda.empty_cache()
+    return {"workload": "BASELINE configs[4]: 1B x 64B keys (CityHash64) split over the N GPUs, device-resident",
+            "keys_total": CONFIG4_KEYS,
+            "scaling": "strong", "steps": steps, "ms_per_step": round(elapsed_max / steps * 1e3, 4),
+            "value": round(value, 4), "unit": "Gkeys/s", "kernel": kernel,
+            "keys_per_gpu": [r["keys"] for r in pr["ranks"]],
+            "aggregate_frac": round(CONFIG4_KEYS * 72.0 / (elapsed_max / steps) / 1e9 / (world * PEAK_HBM_GBPS), 4),
+            "per_gpu_Gkeys_s": pr["Gkeys_s"], "per_gpu_frac": pr["frac"],
+            "per_gpu_event_ms": [r["event_ms"] for r in pr["ranks"]],
+            "parity": parity}
 
 
 def load_traffic(cfg, n, kernel):
@@ -474,87 +576,115 @@ def load_traffic(cfg, n, kernel):
         return None
 
 
+def city64_chunk_fold(folds, first, n):
+    """Reference fold of keys [first, first+n) of the 64-B key stream, summed
+    from the committed 16M-key chunk folds of the 1B-key config (the fold is
+    position-weighted by global index, so chunk folds add); None when the
+    range is not made of whole chunks inside the 1B keys."""
+    c5 = (folds or {}).get("cfg5_city64_1B_x64", {})
+    ch, ck = c5.get("chunks"), int(c5.get("chunk_keys", 16 * M))
+    if not ch or n <= 0 or first % ck or n % ck or (first + n) // ck > len(ch):
+        return None
+    return sum(int(ch[j], 16) for j in range(first // ck, (first + n) // ck)) & ((1 << 64) - 1)
+
+
 def golden_shard_fold(folds, cfg, sh):
     """Reference fold of exactly this shard's keys, when the golden file has it."""
     if folds is None:
         return None, None
     if cfg in ("cfg2", "cfg5"):
-        c5 = folds.get("cfg5_city64_1B_x64", {})
-        if sh.n == 16 * M and sh.first % (16 * M) == 0 and "chunks" in c5:
-            j = sh.first // (16 * M)
-            if j < len(c5["chunks"]):
-                return int(c5["chunks"][j], 16), f"cfg5 chunk {j} (keys {sh.first}..+16M)"
-        if sh.n == 128 * M and sh.first % (128 * M) == 0:
-            j = sh.first // (128 * M)
-            if j < 8:
-                return int(c5["shards"][j], 16), f"cfg5 shard {j}"
-        if sh.first == 0 and sh.n == 16 * M:
-            return int(folds["cfg2_city64_16M_x64"]["total"], 16), "cfg2 total"
+        f = city64_chunk_fold(folds, sh.first, sh.n)
+        if f is not None:
+            return f, f"cfg5 16M-key chunks {sh.first // (16 * M)}..{(sh.first + sh.n) // (16 * M) - 1}"
     if cfg == "long" and sh.n == M and sh.first % M == 0:
         g = folds.get("long_crc128_1M_x1024", {}).get("shards", [])
         if sh.first // M < len(g):
             return int(g[sh.first // M], 16), f"long shard {sh.first // M}"
-    if cfg == "cfg4" and sh.first == 0 and sh.n == 16 * M:
-        return int(folds["cfg4_crc128_16M_x64"]["total"], 16), "cfg4 total"
-    if cfg == "cfg3" and sh.rank == 0 and sh.n == 64 * M:
-        return int(folds["cfg3_city64_64M_mixed"]["total"], 16), "cfg3 total"
+    if cfg == "cfg4" and sh.n == 16 * M and sh.first % (16 * M) == 0:
+        c4 = folds.get("cfg4_crc128_16M_x64", {})
+        r = sh.first // (16 * M)
+        if r == 0:
+            return int(c4["total"], 16), "cfg4 total"
+        if r < len(c4.get("rank_chunks", [])):
+            return int(c4["rank_chunks"][r], 16), f"cfg4 weak shard {r}"
+    if cfg == "cfg3" and sh.n == 64 * M and sh.first == sh.rank * 64 * M:
+        c3 = folds.get("cfg3_city64_64M_mixed", {})
+        if sh.rank == 0:
+            return int(c3["total"], 16), "cfg3 total"
+        if sh.rank < len(c3.get("ranks", [])):
+            return int(c3["ranks"][sh.rank]["fold"], 16), f"cfg3 rank {sh.rank}"
     return None, None
 
 
-def check_parity(P, torch, D, cfg, sh, out, extra, dev):
+# parity status of one shard, combined over ranks by MIN: any failure makes the
+# line FAILED, any shard without a reference fold makes it "unchecked"
+PAR_FAIL, PAR_UNCHECKED, PAR_OK = 0, 1, 2
+PAR_WORD = {PAR_FAIL: "FAILED", PAR_UNCHECKED: "unchecked", PAR_OK: "ok"}
+
+
+def combine_parity(D, status, msgs, world, cdev):
+    """One parity string for the whole job: the worst status over ranks."""
+    worst = D.allreduce_min_int(status, device=cdev)
+    if world > 1:
+        msgs.append(f"worst of {world} ranks: {PAR_WORD[worst]}")
+    return f"{PAR_WORD[worst]}: " + "; ".join(msgs)
+
+
+def check_parity(P, torch, D, cfg, sh, out, extra, cdev):
     """Bit-exact check of this rank's WHOLE shard against the reference golden
     folds (tests/golden/config_folds.json: data generated from the reference
-    city.c by tests/golden/gen_golden.py).  No oracle code runs here; the
-    cpu_baseline leg separately compares the reference's own digests of its
-    sample with this run's GPU digests."""
+    city.c by tests/golden/gen_golden.py).  A shard the golden file has no
+    fold for is reported "unchecked", never "ok".  No oracle code runs here;
+    the cpu_baseline leg separately compares the reference's own digests of
+    its sample with this run's GPU digests."""
     folds = golden_folds()
     if folds is None:
-        return "unchecked (tests/golden/config_folds.json missing)"
-    msgs, ok = [], True
-    if cfg == "cfg1":
-        f = folds.get("cfg1_pdht_hash_1M_x64", {})
-        pl = [x for x in f.get("placements", []) if x["nptes"] == 1 and x["nranks"] == 4]
-        if sh.first == 0 and sh.n == f.get("n") and pl:
-            mb, pt, rk, hist = extra
-            got = {"mbits": D.fold_tensor(mb, 0), "ptindex": D.fold_tensor(pt.to(torch.int64) & 0xFFFFFFFF, 0),
-                   "rank": D.fold_tensor(rk.to(torch.int64) & 0xFFFFFFFF, 0), "hist": D.fold_tensor(hist, 0)}
-            want = {"mbits": f["mbits"], "ptindex": pl[0]["ptindex"], "rank": pl[0]["rank"], "hist": pl[0]["hist"]}
-            bad = [k for k, v in got.items() if v != int(want[k], 16)]
-            ok = not bad
-            msgs.append(f"mbits, ptindex, rank and histogram folds {'==' if ok else '!='} reference golden "
-                        f"(cfg1, nptes 1, nranks 4)" + (f" (mismatch: {bad})" if bad else ""))
+        return combine_parity(D, PAR_UNCHECKED, ["tests/golden/config_folds.json missing"], sh.world, cdev)
+    msgs, st = [], PAR_UNCHECKED
+    if cfg in ("cfg1", "place"):
+        want = None
+        if cfg == "cfg1":
+            f = folds.get("cfg1_pdht_hash_1M_x64", {})
+            pl = [x for x in f.get("placements", []) if x["nptes"] == 1 and x["nranks"] == 4]
+            r = sh.first // M
+            if sh.n == f.get("n") and sh.first % M == 0 and pl:
+                if r == 0:
+                    want = {"mbits": f["mbits"], "ptindex": pl[0]["ptindex"], "rank": pl[0]["rank"],
+                            "hist": pl[0]["hist"]}
+                elif r < len(f.get("ranks", [])):
+                    want = f["ranks"][r]
+            what = f"cfg1 rank {r}, nptes 1, nranks 4"
         else:
-            msgs.append("no golden fold for this shard")
-    elif cfg == "place":
-        r = sh.first // (16 * M)
-        g = folds.get("place_8B_16M", {}).get("shards", [])
-        if sh.n == 16 * M and sh.first % (16 * M) == 0 and r < len(g):
+            r = sh.first // (16 * M)
+            g = folds.get("place_8B_16M", {}).get("shards", [])
+            if sh.n == 16 * M and sh.first % (16 * M) == 0 and r < len(g):
+                want = g[r]
+            what = f"place shard {r}"
+        if want is not None:
             mb, pt, rk, hist = extra
             got = {"mbits": D.fold_tensor(mb, sh.first),
                    "ptindex": D.fold_tensor(pt.to(torch.int64) & 0xFFFFFFFF, sh.first),
                    "rank": D.fold_tensor(rk.to(torch.int64) & 0xFFFFFFFF, sh.first),
                    "hist": D.fold_tensor(hist, 0)}
-            bad = [k for k, v in got.items() if v != int(g[r][k], 16)]
-            ok = not bad
-            msgs.append(f"mbits, ptindex, rank and histogram folds {'==' if ok else '!='} reference "
-                        f"golden (place shard {r})" + (f" (mismatch: {bad})" if bad else ""))
+            bad = [k for k, v in got.items() if v != int(want[k], 16)]
+            st = PAR_FAIL if bad else PAR_OK
+            msgs.append(f"mbits, ptindex, rank and histogram folds {'!=' if bad else '=='} reference golden "
+                        f"({what})" + (f" (mismatch: {bad})" if bad else ""))
         else:
-            msgs.append("no golden fold for this shard")
+            msgs.append(f"rank {sh.rank}: no reference fold for keys {sh.first}..+{sh.n}")
     else:
         want, what = golden_shard_fold(folds, cfg, sh)
         if want is not None:
             first_idx = 2 * sh.first if cfg in ("cfg4", "long") else sh.first
-            ok = D.fold_tensor(out, first_idx) == want
-            msgs.append(f"full-shard fold {'==' if ok else '!='} reference golden ({what})")
+            good = D.fold_tensor(out, first_idx) == want
+            st = PAR_OK if good else PAR_FAIL
+            msgs.append(f"full-shard fold {'==' if good else '!='} reference golden ({what})")
         else:
-            msgs.append("no golden fold for this shard")
-    all_ok = D.allreduce_min_flag(bool(ok), device=dev)
-    if sh.world > 1:
-        msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
-    return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
+            msgs.append(f"rank {sh.rank}: no reference fold for keys {sh.first}..+{sh.n}")
+    return combine_parity(D, st, msgs, sh.world, cdev)
 
 
-def check_buckets(P, torch, D, sh, keys, b, dev):
+def check_buckets(P, torch, D, sh, keys, b, dev, cdev):
     """Bucketing checks without oracle code: the whole shard's bucketed mbits,
     original indices and bucket offsets against the reference golden folds
     (bucket config), and full-size properties on the device -- index is a
@@ -562,7 +692,7 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
     keys_out == keys[index], mbits == CityHash64(keys_out)."""
     nr, ko, mb, ix, offs = b["nranks"], b["ko"], b["mb"], b["ix"], b["offs"]
     n = ix.numel()
-    msgs, ok = [], True
+    msgs, ok, golden = [], True, False
     folds = golden_folds() or {}
     g = folds.get("bucket_8B_16M" if nr == 1024 else f"bucket_8B_16M_{nr}", {})
     r = sh.first // (16 * M)
@@ -570,9 +700,11 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
         gs = g["shards"][r]
         got = {"mbits": D.fold_tensor(mb, 0), "index": D.fold_tensor(ix, 0), "offsets": D.fold_tensor(offs, 0)}
         bad = [k for k, v in got.items() if v != int(gs[k], 16)]
-        ok = not bad
+        ok, golden = not bad, True
         msgs.append(f"bucketed mbits, index and offsets folds {'==' if ok else '!='} reference golden "
                     f"(bucket shard {r})" + (f" (mismatch: {bad})" if bad else ""))
+    else:
+        msgs.append(f"rank {sh.rank}: no reference fold for this bucketing (properties only)")
     ix = ix.long() & 0xFFFFFFFF
     srt = torch.sort(ix).values
     perm = bool((srt == torch.arange(n, device=dev)).all().item())
@@ -596,13 +728,11 @@ def check_buckets(P, torch, D, sh, keys, b, dev):
             mine = mine and bool((xk[j].view(torch.int64) == want).all().item())
         msgs.append(f"exchange: {xi.numel()} keys received, all owned by this rank {'ok' if mine else 'FAILED'}")
         ok = ok and mine
-    all_ok = D.allreduce_min_flag(ok, device=dev)
-    if sh.world > 1:
-        msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
-    return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
+    st = PAR_FAIL if not ok else (PAR_OK if golden else PAR_UNCHECKED)
+    return combine_parity(D, st, msgs, sh.world, cdev)
 
 
-def check_records(P, torch, D, sh, keys, b, dev):
+def check_records(P, torch, D, sh, keys, b, dev, cdev):
     """Record bucketing checks without oracle code: the records' mbits and
     source-index columns and the bucket offsets against the same reference
     golden folds as the array form (bucket config), and full-size properties:
@@ -612,16 +742,18 @@ def check_records(P, torch, D, sh, keys, b, dev):
     n = rec.shape[0]
     ty, sr, hi, ix32, mb, ko = P.record_fields(rec, keys.shape[1])
     ix = ix32.to(torch.int64) & 0xFFFFFFFF
-    msgs, ok = [], True
+    msgs, ok, golden = [], True, False
     g = (golden_folds() or {}).get("bucket_8B_16M", {})
     r = sh.first // (16 * M)
     if nr == g.get("nranks") and n == g.get("n") and sh.first % n == 0 and r < len(g.get("shards", [])):
         gs = g["shards"][r]
         got = {"mbits": D.fold_tensor(mb, 0), "index": D.fold_tensor(ix, 0), "offsets": D.fold_tensor(offs, 0)}
         bad = [k for k, v in got.items() if v != int(gs[k], 16)]
-        ok = not bad
+        ok, golden = not bad, True
         msgs.append(f"records' mbits, index and offsets folds {'==' if ok else '!='} reference golden "
                     f"(bucket shard {r})" + (f" (mismatch: {bad})" if bad else ""))
+    else:
+        msgs.append(f"rank {sh.rank}: no reference fold for this bucketing (properties only)")
     perm = bool((torch.sort(ix).values == torch.arange(n, device=dev)).all().item())
     same = bool((ko == keys[ix]).all().item()) and bool((P.city64_batch(ko.contiguous()) == mb).all().item())
     hdr = bool(((ty == P.PDHT_PUT) & (sr == sh.rank) & (hi == 0)).all().item())
@@ -644,13 +776,11 @@ def check_records(P, torch, D, sh, keys, b, dev):
             mine = mine and bool((xk[j].contiguous().view(torch.int64) == want).all().item())
         msgs.append(f"exchange: {xr.shape[0]} records received, all owned by this rank {'ok' if mine else 'FAILED'}")
         ok = ok and mine
-    all_ok = D.allreduce_min_flag(ok, device=dev)
-    if sh.world > 1:
-        msgs.append(f"all {sh.world} ranks {'ok' if all_ok else 'NOT ok'}")
-    return ("ok: " if all_ok else "FAILED: ") + "; ".join(msgs)
+    st = PAR_FAIL if not ok else (PAR_OK if golden else PAR_UNCHECKED)
+    return combine_parity(D, st, msgs, sh.world, cdev)
 
 
-def host_rate(P, torch, n, cfg, D, dev):
+def host_rate(P, torch, n, cfg, D, dev, cdev):
     """Host-resident rate: pinned keys in, pinned digests out, through the
     C-ABI host entry point (zero-copy for pinned buffers; PCIe-bound).  At
     N > 1 every rank runs at the same time on its own GPU (its own PCIe
@@ -677,7 +807,7 @@ def host_rate(P, torch, n, cfg, D, dev):
         res = {"value": mine["Gkeys_s"], "unit": "Gkeys/s", "keys": m, "GBps_pcie": mine["GBps_pcie"],
                "note": "pinned host keys and digests; the kernel reads/writes them over PCIe (zero-copy)"}
         if world > 1:
-            dtmax = D.allreduce_max([dt], device=dev)[0]
+            dtmax = D.allreduce_max([dt], device=cdev)[0]
             allr = [None] * world
             dist.all_gather_object(allr, mine)
             res.update(value=round(m * world / dtmax / 1e9, 4), keys=m * world,

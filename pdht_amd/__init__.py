@@ -405,17 +405,24 @@ def city64_seed_batch(keys, seed: int, out=None, stream=None):
     return city64_seeds_batch(keys, K2, seed, out, stream)
 
 
-def _check_var(data, offsets, check=True):
-    """(n, nbytes): nbytes = the data buffer's size, the bound of the key
-    bytes the batch spans (sizes the kernel's LDS window; never addresses).
-    check: also read offsets[0] and offsets[n] back (one 16-B D2H copy, which
-    synchronises with the stream) and require 0 <= offsets[0] <= offsets[n]
-    <= data.numel(), so that a bad offsets tensor raises instead of sending
-    the window kernel past the data buffer.  Skipped while the stream is being
-    captured into a graph, and with check=False (the caller vouches for the
-    offsets, e.g. a timed loop over offsets it has already checked); the
-    kernels trust that offsets never decrease, as the reference trusts its key
-    pointers."""
+def _check_var(data, offsets, check=True, stream=None):
+    """(n, nbytes) of a variable-length batch.  nbytes is what the C ABI takes
+    as the key bytes the batch spans: it picks the LDS window and how the
+    batch is cut into ~512 MiB launches (launch.h launch_var); it never
+    addresses memory.
+
+    check=True (default): read offsets[0] and offsets[n] back ON THE LAUNCH
+    STREAM (`stream`, else the device's current stream) -- one 16-B D2H copy
+    that waits for the work queued before it on that stream, so this call is
+    host-synchronous -- require 0 <= offsets[0] <= offsets[n] <= data.numel()
+    (a bad offsets tensor raises instead of sending the window kernel past the
+    data buffer) and pass the exact span offsets[n] - offsets[0].
+    check=False, or while the launch stream is being captured into a graph:
+    no read, fully asynchronous; the caller vouches for the offsets and the
+    span passed is data.numel() (an upper bound; a much larger buffer than
+    the keys only skews the window/launch-size heuristic, never correctness).
+    The kernels trust that offsets never decrease, as the reference trusts
+    its key pointers."""
     torch = _torch()
     if data.dtype != torch.uint8 or not data.is_cuda or not data.is_contiguous():
         raise ValueError("data must be a contiguous CUDA uint8 tensor")
@@ -423,15 +430,21 @@ def _check_var(data, offsets, check=True):
     if offsets.dim() != 1 or offsets.numel() < 1:
         raise ValueError("offsets must be a 1-D int64 tensor of n+1 entries")
     n = offsets.numel() - 1
-    if check and n and not torch.cuda.is_current_stream_capturing():
-        lo, hi = (int(x) for x in offsets[[0, n]].tolist())
-        if not 0 <= lo <= hi <= data.numel():
-            raise ValueError(f"offsets span bytes [{lo}, {hi}) but data holds {data.numel()}")
+    if check and n:
+        s = stream if stream is not None else torch.cuda.current_stream(data.device)
+        if s.device != data.device:
+            raise ValueError(f"stream is on {s.device}, tensors on {data.device}")
+        with torch.cuda.stream(s):
+            if not torch.cuda.is_current_stream_capturing():
+                lo, hi = (int(x) for x in offsets[[0, n]].tolist())
+                if not 0 <= lo <= hi <= data.numel():
+                    raise ValueError(f"offsets span bytes [{lo}, {hi}) but data holds {data.numel()}")
+                return n, hi - lo
     return n, data.numel()
 
 
 def city64_var_batch(data, offsets, out=None, stream=None, check=True):
-    n, nb = _check_var(data, offsets, check)
+    n, nb = _check_var(data, offsets, check, stream)
     out = _out(n, 1, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_city64_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
@@ -458,7 +471,7 @@ def city128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
 
 
 def city128_var_batch(data, offsets, out=None, stream=None, check=True):
-    n, nb = _check_var(data, offsets, check)
+    n, nb = _check_var(data, offsets, check, stream)
     out = _out(n, 2, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_city128_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),
@@ -485,7 +498,7 @@ def citycrc128_seed_batch(keys, seed: tuple[int, int], out=None, stream=None):
 
 
 def citycrc128_var_batch(data, offsets, out=None, stream=None, check=True):
-    n, nb = _check_var(data, offsets, check)
+    n, nb = _check_var(data, offsets, check, stream)
     out = _out(n, 2, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_citycrc128_batch_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out),
@@ -709,7 +722,7 @@ def key_stream(keys, out=None, stream=None):
 
 def key_stream_var(data, offsets, out=None, stream=None, check=True):
     """Calibration: the variable-length kernel's data movement with an XOR fold."""
-    n, nb = _check_var(data, offsets, check)
+    n, nb = _check_var(data, offsets, check, stream)
     out = _out(n, 1, data.device, out)
     with _on(data.device, stream) as g:
         _check(lib().pdht_hip_key_stream_var_dev(_dptr(data), nb, _dptr(offsets), n, _dptr(out), g.stream),

@@ -51,8 +51,13 @@ def fold_tensor(d, first_index: int) -> int:
     passes first_index = 2*first_key)."""
     import torch
     d = d.reshape(-1)
-    idx = torch.arange(d.numel(), device=d.device, dtype=torch.int64) + first_index
-    return int((d * (2 * idx + 1)).sum().item()) & MASK64
+    acc = torch.zeros((), dtype=torch.int64, device=d.device)
+    step = 1 << 24  # bounded temporaries: a 1B-key shard folds in 16M-entry pieces
+    for lo in range(0, d.numel(), step):
+        part = d[lo:lo + step]
+        idx = torch.arange(part.numel(), device=d.device, dtype=torch.int64) + (first_index + lo)
+        acc += (part * (2 * idx + 1)).sum()  # int64 arithmetic wraps mod 2^64
+    return int(acc.item()) & MASK64
 
 
 def _to_signed(v: int) -> int:
@@ -78,6 +83,16 @@ def allreduce_max(values, device=None) -> list[float]:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.tolist()]
+
+
+def allreduce_min_int(v: int, device=None) -> int:
+    """Min over ranks of a small integer (the bench's per-shard parity status)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(v)], dtype=torch.int64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
 
 
 def allreduce_min_flag(ok: bool, device=None) -> bool:
@@ -167,8 +182,8 @@ def per_rank_report(rank: int, local: int, world: int, n: int, bytes_per_key: fl
     Gkeys/s and roofline fraction per GPU, plus the world (SURVEY.md §8e:
     per-GPU and aggregate Gkeys/s at 1/2/4/8 GPUs)."""
     import torch.distributed as dist
-    mine = dict(rank=rank, local_rank=local, **device_info(device),
-                kernel_ms=round(kernel_ms, 4),
+    mine = dict(rank=rank, local_rank=local, **device_info(device), keys=n,
+                event_ms=round(kernel_ms, 4),
                 Gkeys_s=round(n / (kernel_ms / 1e3) / 1e9, 3),
                 frac=round(bytes_per_key * n / (kernel_ms / 1e3) / 1e9 / peak_GBps, 4),
                 wall_Gkeys_s=round(n * steps / elapsed_s / 1e9, 3))

@@ -17,6 +17,8 @@ the two modulo reductions of hash.c:27 and :29 done in Python.
   python tests/golden/gen_golden.py --r02    # + WeakHashLen32WithSeeds(6) vectors
   python tests/golden/gen_golden.py --bucket8k  # + 8192-rank bucketing folds
                                              #   and cfg1 pdht_hash placement folds (added)
+  python tests/golden/gen_golden.py --multirank # + per-rank cfg1/cfg3/cfg4 folds of the
+                                             #   N > 1 weak-scaling shards (added)
 """
 from __future__ import annotations
 
@@ -281,6 +283,48 @@ def cfg1_folds() -> dict:
     return res
 
 
+def folds_multirank(ranks: int = 8) -> dict:
+    """Per-rank folds of the bench's weak-scaling shards at N > 1, for every
+    rank r < 8 (so every world size 1/2/4/8 can check each of its ranks):
+      cfg3  rank r: 64M mixed keys, lengths from the lengths stream at key
+            r*64M, bytes from the key stream at word r << 40 (bench.py's
+            disjoint segment); fold at global index r*64M;
+      cfg4  rank r: keys [r*16M, (r+1)*16M), CityHashCrc128, fold over the
+            interleaved {lo,hi} array at index 2*r*16M;
+      cfg1  rank r: keys [r*1M, (r+1)*1M), pdht_hash with nptes 1, nranks 4:
+            folds of mbits, ptindex, rank (global index) and the histogram."""
+    thr = os.cpu_count() or 8
+    out = {"cfg3": [], "cfg4": [], "cfg1": []}
+    n3 = 64 * M
+    for r in range(ranks):
+        lens = O.mixed_lengths(n3, first_key=r * n3)
+        offs = np.zeros(n3 + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        del lens
+        total = int(offs[-1])
+        data = O.splitmix64(O.SEED_KEYS, r << 40, (total + 7) // 8).view(np.uint8)[:total]
+        d = O.apply_ref64(data, n3, offsets=offs, threads=thr)
+        out["cfg3"].append({"total_bytes": total, "fold": f"{O.fold64(d, r * n3):016x}"})
+        del data, offs, d
+        print(f"  cfg3 rank {r}: {out['cfg3'][-1]}", flush=True)
+    n4 = 16 * M
+    for r in range(ranks):
+        keys = O.fixed_keys(n4, 64, first_key=r * n4)
+        d = O.apply_ref128(keys, n4, L=64, threads=thr, fn_name="CityHashCrc128")
+        out["cfg4"].append(f"{O.fold64(d.reshape(-1), 2 * r * n4):016x}")
+        print(f"  cfg4 rank {r}: {out['cfg4'][-1]}", flush=True)
+    n1 = M
+    for r in range(ranks):
+        keys = O.fixed_keys(n1, 64, first_key=r * n1)
+        m = O.apply_ref64(keys, n1, L=64, threads=thr)
+        pt = (m % np.uint64(1)).astype(np.uint64)
+        rk = (m % np.uint64(4)).astype(np.uint64)
+        hist = np.bincount(rk.astype(np.int64), minlength=4).astype(np.uint64)
+        out["cfg1"].append({"mbits": f"{O.fold64(m, r * n1):016x}", "ptindex": f"{O.fold64(pt, r * n1):016x}",
+                            "rank": f"{O.fold64(rk, r * n1):016x}", "hist": f"{O.fold64(hist, 0):016x}"})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true")
@@ -290,11 +334,25 @@ def main():
                     help="add the WeakHash vectors (npz) and the cfg1 placement folds (json)")
     ap.add_argument("--bucket8k", action="store_true",
                     help="add the 8192-rank bucketing folds (json)")
+    ap.add_argument("--multirank", action="store_true",
+                    help="add per-rank cfg1/cfg3/cfg4 folds of the N > 1 weak-scaling shards (json)")
     a = ap.parse_args()
     O.build()
     R = O.ref()
     if R is None:
         sys.exit("oracle/_ref not built: /root/reference is required to regenerate fixtures")
+    if a.multirank:
+        path = os.path.join(HERE, "config_folds.json")
+        with open(path) as f:
+            doc = json.load(f)
+        mr = folds_multirank()
+        doc["configs"]["cfg3_city64_64M_mixed"]["ranks"] = mr["cfg3"]
+        doc["configs"]["cfg4_crc128_16M_x64"]["rank_chunks"] = mr["cfg4"]
+        doc["configs"]["cfg1_pdht_hash_1M_x64"]["ranks"] = mr["cfg1"]
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print("added per-rank cfg1/cfg3/cfg4 folds")
+        return
     if a.bucket8k:
         path = os.path.join(HERE, "config_folds.json")
         with open(path) as f:

@@ -40,6 +40,53 @@ def test_gpus_2_launches_two_ranks():
     assert sorted(x["local_rank"] for x in r["ranks"]) == [0, 1]
     pids = {x["pid"] for x in r["ranks"]}
     assert len(pids) == 2                       # two processes, one per rank
+    # the default N > 1 run also times BASELINE configs[4]: 1B x 64 B keys split
+    # over the ranks (strong scaling), beside the cfg2 weak-scaling value
+    c4 = r["plan"]["config4"]
+    assert r["plan"]["config"] == "cfg2" and r["plan"]["value_scaling"] == "weak"
+    assert c4["keys_total"] == 1 << 30 and c4["keys_per_rank"] == [1 << 29, 1 << 29]
+
+
+def test_config4_split_is_whole_reference_chunks():
+    """Every world size the driver runs (1/2/4/8) splits the 1B keys into
+    whole 16M-key chunks, so every rank's slice has a reference fold."""
+    sys.path.insert(0, ROOT)
+    import bench
+    folds = bench.golden_folds()
+    for world in (1, 2, 4, 8):
+        a = type("A", (), {"config": "cfg2", "no_config4": False, "keys_per_gpu": 0, "dist_backend": "nccl"})
+        per = bench.plan(a, world)["config4"]["keys_per_rank"]
+        assert sum(per) == 1 << 30
+        first = 0
+        for n in per:
+            assert bench.city64_chunk_fold(folds, first, n) is not None
+            first += n
+    # the folds of the 8 shards of 1B, summed from chunks, equal the shard folds
+    c5 = folds["cfg5_city64_1B_x64"]
+    for s in range(8):
+        assert bench.city64_chunk_fold(folds, s << 27, 1 << 27) == int(c5["shards"][s], 16)
+    assert bench.city64_chunk_fold(folds, 0, 1 << 30) == int(c5["total"], 16)
+    assert bench.city64_chunk_fold(folds, 5, 1 << 24) is None      # not whole chunks
+    assert bench.city64_chunk_fold(folds, 0, (1 << 30) + (1 << 24)) is None
+
+
+def test_config4_block_only_on_default_workload():
+    sys.path.insert(0, ROOT)
+    import bench
+    mk = lambda **kw: type("A", (), {"config": "cfg2", "no_config4": False, "keys_per_gpu": 0,  # noqa: E731
+                                     "dist_backend": "nccl", **kw})
+    assert "config4" in bench.plan(mk(), 1)
+    assert "config4" not in bench.plan(mk(config="cfg3"), 2)
+    assert "config4" not in bench.plan(mk(no_config4=True), 2)
+    assert "config4" not in bench.plan(mk(keys_per_gpu=1000), 2)
+
+
+def test_gloo_rehearsal_flag_accepted():
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-backend", "gloo", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    (r,) = _json_lines(p.stdout)
+    assert r["plan"]["backend"] == "gloo" and r["world_size"] == 2
 
 
 def test_gpus_1_stays_single_process():

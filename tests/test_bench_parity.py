@@ -1,0 +1,69 @@
+"""bench.py's parity strings: a shard is "ok" only when its digests were
+compared with a reference fold and matched; a shard the golden file has no
+fold for is "unchecked" (never "ok"); a mismatch is "FAILED".  Runs on CPU
+tensors with no process group (world 1)."""
+import sys
+
+import torch
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from pdht_amd import dist as D  # noqa: E402
+
+
+def _shard(first, n, rank=0, world=1):
+    return D.Shard(rank, world, first, n)
+
+
+def test_shard_without_golden_fold_is_unchecked():
+    out = torch.arange(1000, dtype=torch.int64)
+    for cfg in ("cfg2", "cfg3", "cfg4", "cfg5", "long"):
+        p = bench.check_parity(None, torch, D, cfg, _shard(0, 1000), out, None, None)
+        assert p.startswith("unchecked: "), p
+        assert "no reference fold" in p and not p.startswith("ok")
+    # cfg3 rank 9 of a weak-scaling run: no per-rank fold committed
+    p = bench.check_parity(None, torch, D, "cfg3", _shard(9 * 64 * bench.M, 64 * bench.M, rank=9), out, None, None)
+    assert p.startswith("unchecked: "), p
+
+
+def test_wrong_digests_fail(monkeypatch):
+    out = torch.arange(16, dtype=torch.int64)
+    right = D.fold_tensor(out, 0)
+    folds = {"cfg5_city64_1B_x64": {"chunk_keys": 16, "chunks": [f"{(right + 1) & D.MASK64:016x}"]}}
+    monkeypatch.setattr(bench, "golden_folds", lambda: folds)
+    p = bench.check_parity(None, torch, D, "cfg2", _shard(0, 16), out, None, None)
+    assert p.startswith("FAILED: "), p
+
+
+def test_matching_digests_ok(monkeypatch):
+    out = torch.arange(32, dtype=torch.int64) * 0x9E3779B97F4A7C15
+    folds = {"cfg5_city64_1B_x64": {"chunk_keys": 16,
+                                    "chunks": [f"{D.fold_tensor(out[:16], 0):016x}",
+                                               f"{D.fold_tensor(out[16:], 16):016x}"]}}
+    monkeypatch.setattr(bench, "golden_folds", lambda: folds)
+    assert bench.check_parity(None, torch, D, "cfg2", _shard(0, 32), out, None, None).startswith("ok: ")
+    # the second chunk alone, as rank 1 of a 2-way split would hold it
+    assert bench.check_parity(None, torch, D, "cfg2", _shard(16, 16, rank=1, world=1), out[16:], None,
+                              None).startswith("ok: ")
+
+
+def test_committed_multirank_folds_present():
+    """The per-rank folds that make cfg1/cfg3/cfg4 ranks 1..7 checkable."""
+    f = bench.golden_folds()
+    assert len(f["cfg3_city64_64M_mixed"]["ranks"]) == 8
+    assert f["cfg3_city64_64M_mixed"]["ranks"][0]["fold"] == f["cfg3_city64_64M_mixed"]["total"]
+    assert len(f["cfg4_crc128_16M_x64"]["rank_chunks"]) == 8
+    assert f["cfg4_crc128_16M_x64"]["rank_chunks"][0] == f["cfg4_crc128_16M_x64"]["total"]
+    r0 = f["cfg1_pdht_hash_1M_x64"]["ranks"][0]
+    pl = [x for x in f["cfg1_pdht_hash_1M_x64"]["placements"] if (x["nptes"], x["nranks"]) == (1, 4)][0]
+    assert r0["mbits"] == f["cfg1_pdht_hash_1M_x64"]["mbits"]
+    assert (r0["ptindex"], r0["rank"], r0["hist"]) == (pl["ptindex"], pl["rank"], pl["hist"])
+    for w in (2, 4, 8):
+        for r in range(w):
+            sh = D.weak_shard(r, w, 64 * bench.M)
+            assert bench.golden_shard_fold(f, "cfg3", sh)[0] is not None
+            sh = D.weak_shard(r, w, 16 * bench.M)
+            assert bench.golden_shard_fold(f, "cfg4", sh)[0] is not None
+            assert bench.golden_shard_fold(f, "cfg2", sh)[0] is not None

@@ -119,7 +119,7 @@ def test_two_rank_gloo_shards_and_reductions(oracle):
         pr = r["per_rank"]                              # every rank sees every rank's numbers
         assert pr["world_size"] == WORLD and pr["backend"] == "gloo"
         assert [x["rank"] for x in pr["ranks"]] == list(range(WORLD))
-        assert all({"host", "device", "name", "pci", "kernel_ms", "Gkeys_s", "frac", "wall_Gkeys_s"} <= set(x)
+        assert all({"host", "device", "name", "pci", "event_ms", "keys", "Gkeys_s", "frac", "wall_Gkeys_s"} <= set(x)
                    for x in pr["ranks"])
         assert pr["Gkeys_s"] == [round((1 << 20) / (k + 1) / 1e6, 3) for k in range(WORLD)]
         assert pr["frac"] == [round(72 * (1 << 20) / (k + 1) / 1e6 / 8000, 4) for k in range(WORLD)]

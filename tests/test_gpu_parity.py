@@ -160,18 +160,25 @@ def test_seeded_batches(dev, oracle, L):
     assert [tuple(int(x) for x in g) for g in got] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k]
 
 
+def _variants(vs):
+    """Variant 0 is the product library; any other variant loads the tuning
+    build and runs only with --tuning (conftest.py), so the default -m gpu run
+    loads libpdht_hip.so / libpdht_hip_mpi.so only."""
+    return [v if v == 0 else pytest.param(v, marks=pytest.mark.tuning) for v in vs]
+
+
 VARIANT_KERNELS = {0: "k_fixed_xpose64<nt,d2>@3", 7: "k_fixed_xpose64<nt,d1>@4",
                    26: "k_fixed_xpose64<nt-load,plain-store,d2>@3"}
 
 
-@pytest.mark.parametrize("variant", sorted(VARIANT_KERNELS))
+@pytest.mark.parametrize("variant", _variants(sorted(VARIANT_KERNELS)))
 def test_64B_kernel_variants_bitexact(dev, oracle, variant):
     """The product kernel, and the tuning build's alternatives (A/B only)."""
     n = M + 13
     k = oracle.fixed_keys(n, 64)
     want = oracle.city64_fixed(k)
     kd = to_dev(k, dev)
-    with P.tuning(variant):
+    with P.tuning(variant) if variant else _nullctx():
         got = u64(P.city64_batch(kd))
         kern = P.last_kernel()
         got128 = u64(P.citycrc128_batch(kd[:100000]))
@@ -279,7 +286,7 @@ def auto_var_kernel(total_bytes, n):
     return "k_window<var,nt,16K>@2" if total_bytes // n > 160 else "k_window<var,nt,10224>@4"
 
 
-@pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
+@pytest.mark.parametrize("variant", _variants(sorted(VAR_KERNELS)))
 def test_var_edge_cases(dev, oracle, variant):
     with P.tuning(variant) if variant else _nullctx():
         total, n = _var_edge_cases(dev, oracle)
@@ -295,7 +302,7 @@ class _nullctx:
         return False
 
 
-@pytest.mark.parametrize("variant", sorted(VAR_KERNELS))
+@pytest.mark.parametrize("variant", _variants(sorted(VAR_KERNELS)))
 def test_var_many_tiles_per_wave(dev, oracle, variant):
     """Enough keys that every wave of the persistent grid runs several tiles,
     with a few keys longer than any window and empty keys sprinkled in (runs
@@ -551,8 +558,8 @@ def test_bucket_batch(dev, oracle, L, nranks, n, variant):
     assert (offs.cpu().numpy() == want_offs).all()
 
 
-@pytest.mark.parametrize("L,nranks,variant", [(L, nr, v) for L in (8, 16, 32) for nr in (1000, 8192)
-                                               for v in (0, 70)])
+@pytest.mark.parametrize("L,nranks,variant", _tuning_marked([(L, nr, v) for L in (8, 16, 32)
+                                                              for nr in (1000, 8192) for v in (0, 70)]))
 def test_bucket_skewed(dev, oracle, L, nranks, variant):
     """Few distinct keys: whole batches land in a handful of buckets, so the
     two-pass sort meets segments far longer than its 4096-key sub-tiles and
@@ -652,10 +659,6 @@ def test_host_resident_paths(dev, oracle):
     op = torch.empty(n, dtype=torch.int64).pin_memory()
     P.city64_batch_host(kp, out=op)  # pinned in and out: zero-copy kernel
     assert (op.numpy().view(np.uint64) == want).all()
-    op.zero_()
-    with P.tuning(61):  # pinned, through the chunked copy pipeline (A/B)
-        P.city64_batch_host(kp, out=op)
-    assert (op.numpy().view(np.uint64) == want).all()
     # zero-copy on pointers inside pinned allocations (offset rows)
     op2 = torch.zeros(n - 7, dtype=torch.int64).pin_memory()
     P.city64_batch_host(kp[7:], out=op2)
@@ -686,6 +689,19 @@ def test_host_resident_paths(dev, oracle):
     outs = (pinned(len(k8), np.uint64), pinned(len(k8), np.uint32), pinned(len(k8), np.uint32))
     P.place_batch_host(pk8, 3, 12, out=outs)
     assert (outs[0] == m2).all() and (outs[1] == p2).all() and (outs[2] == r2).all()
+
+
+@pytest.mark.tuning
+def test_host_pinned_through_copy_pipeline(dev, oracle):
+    """Tuning variant 61: pinned buffers forced through the chunked copy
+    pipeline (the A/B of zero-copy against staging)."""
+    n = 2 * M + 5
+    k = oracle.fixed_keys(n, 64)
+    kp = torch.from_numpy(k).pin_memory()
+    op = torch.zeros(n, dtype=torch.int64).pin_memory()
+    with P.tuning(61):
+        P.city64_batch_host(kp, out=op)
+    assert (op.numpy().view(np.uint64) == oracle.city64_fixed(k)).all()
 
 
 def test_zero_copy_misaligned_var_keys(dev, oracle):
@@ -736,7 +752,7 @@ def test_cfg4_crc128_16M_full_fold(dev, folds):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
-@pytest.mark.parametrize("variant", [0, 13, 118])
+@pytest.mark.parametrize("variant", _variants([0, 13, 118]))
 def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     """8.7 GB of keys: offsets far past 2^31 and 2^32 (64-bit window math)."""
     f = folds["cfg3_city64_64M_mixed"]
@@ -904,7 +920,7 @@ def test_batches_capture_in_hip_graph(dev, oracle):
         assert (bk[3].cpu().numpy().view(np.uint32) == order).all() and (u64(bk[1]) == m2[order]).all()
 
 
-@pytest.mark.parametrize("variant", [0, 114])
+@pytest.mark.parametrize("variant", _variants([0, 114]))
 def test_chunked_launches(dev, oracle, variant):
     """Batches past launch_chunk_bytes() go out as consecutive launches (512
     MiB in the product, 256 MiB in tuning variant 114): fixed keys (digests,
@@ -941,3 +957,40 @@ def test_chunked_launches(dev, oracle, variant):
         dv = u64(P.city64_var_batch(data, offs))
     dh, oh = data.cpu().numpy(), offs.cpu().numpy().astype(np.uint64)
     assert (dv == oracle.city64_var(dh, oh)).all()
+
+
+def test_var_offsets_check_on_launch_stream(dev, oracle):
+    """The variable-length wrappers' default offsets check reads offsets[0] /
+    offsets[n] on the LAUNCH stream: offsets written on a side
+    stream are seen, bad ones raise, and capture on that side stream skips
+    the host read (the captured call replays correctly)."""
+    data, offs = oracle.mixed_keys(20000)
+    want = oracle.city64_var(data, offs)
+    s = torch.cuda.Stream(device=dev)
+    dd = to_dev(data, dev)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        od = torch.zeros(offs.size, dtype=torch.int64, device=dev)
+        od.copy_(torch.from_numpy(offs.astype(np.int64)).pin_memory(), non_blocking=True)
+        bad = od.clone()
+        bad[-1] = data.size + 1
+    got = P.city64_var_batch(dd, od, stream=s)
+    s.synchronize()
+    assert (u64(got) == want).all()
+    with pytest.raises(ValueError, match="offsets span"):
+        P.city64_var_batch(dd, bad, stream=s)
+    out = torch.zeros(offs.size - 1, dtype=torch.int64, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        P.city64_var_batch(dd, od, out=out, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert (u64(out) == want).all()
+
+
+def test_default_run_loads_product_libraries_only(request):
+    """Runs last: without --tuning no test has opened the tuning build."""
+    if request.config.getoption("--tuning"):
+        pytest.skip("tuning run")
+    maps = open("/proc/self/maps").read()
+    assert "libpdht_hip_tuning.so" not in maps

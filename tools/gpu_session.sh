@@ -27,7 +27,7 @@ for step in "$@"; do
              tail -15 gpurun_out/gpu_ktests.log | cut -c1-300 ;;
     smoke)   timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log; rc=$?
              tail -1 gpurun_out/smoke.log ;;
-    bench)   timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
+    bench)   timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
              tail -1 gpurun_out/bench.log | cut -c1-600 ;;
     bench_*) cfg=${step#bench_}
              timeout -k 10 300 python bench.py --config $cfg > "gpurun_out/$step.log" 2>&1; rc=$?
@@ -52,6 +52,9 @@ for step in "$@"; do
              # SQ counters of the A/B harness's variants (one rocprofv3 pass; kernels told apart by name)
              timeout -s KILL 200 rocprofv3 --pmc ${PMCS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS} --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sqab_$w" -o run --output-format csv -- python3 tools/abbench.py --work $w --variants ${VARIANTS:-0} --rounds 1 --reps 3 > gpurun_out/sqab_$w.log 2>&1; rc=$?
              python3 tools/pmc_summary.py gpurun_out/sqab_$w/run_counter_collection.csv ;;
+    rehearse2) # the N = 2 path end to end on one GPU: 2 ranks, gloo collectives, both ranks on device 0
+             timeout -k 10 500 python bench.py --gpus 2 --dist-backend gloo > gpurun_out/rehearse2.log 2>&1; rc=$?
+             tail -1 gpurun_out/rehearse2.log | cut -c1-900 ;;
     torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-host > gpurun_out/torchrun1.log 2>&1; rc=$?
              tail -1 gpurun_out/torchrun1.log | cut -c1-600 ;;
     *) echo "unknown step $step"; rc=0 ;;
