@@ -444,7 +444,7 @@ def main():
             extra = (*P.place_batch(keys, *((1, 4) if cfg == "cfg1" else (3, 1024)), hist=hist), hist)
         if cfg == "cfg2r":
             ps = [check_parity(P, torch, D, "cfg2", sh, r, None, cdev) for r in rot]
-            worst = min(ps, key=lambda p: list(PAR_WORD.values()).index(p.split(":")[0]))
+            worst = min(ps, key=lambda p: list(PAR_WORD.values()).index(parity_word(p)))
             parity = worst + f" (all {len(rot)} rotating digest buffers)"
         else:
             parity = check_parity(P, torch, D, cfg, sh, out, extra, cdev)
@@ -496,9 +496,9 @@ def main():
         c4 = config4_block(P, torch, D, a, rank, local, world, dev, cdev)
         if rank == 0:
             res["baseline_config4"] = c4
-            w4 = c4["parity"].split(":")[0]
-            if w4 != "ok" and res["parity"].startswith("ok"):
-                res["parity"] = f"{w4}: " + res["parity"][4:] + " | configs[4] block: " + c4["parity"]
+            w4 = parity_word(c4["parity"])
+            if w4 != "ok" and parity_word(res["parity"]) == "ok":  # the line says the worst of both
+                res["parity"] = f"{w4}: " + res["parity"] + " | configs[4] block: " + c4["parity"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -622,11 +622,20 @@ PAR_FAIL, PAR_UNCHECKED, PAR_OK = 0, 1, 2
 PAR_WORD = {PAR_FAIL: "FAILED", PAR_UNCHECKED: "unchecked", PAR_OK: "ok"}
 
 
+def parity_word(p: str) -> str:
+    """"ok" / "unchecked" / "FAILED": the first word of a parity string."""
+    return p.split()[0].rstrip(":")
+
+
 def combine_parity(D, status, msgs, world, cdev):
-    """One parity string for the whole job: the worst status over ranks."""
+    """One parity string for the whole job: the worst status over ranks, and
+    every rank's own finding (gathered, in rank order)."""
     worst = D.allreduce_min_int(status, device=cdev)
     if world > 1:
-        msgs.append(f"worst of {world} ranks: {PAR_WORD[worst]}")
+        import torch.distributed as dist
+        allm = [None] * world
+        dist.all_gather_object(allm, f"[rank {dist.get_rank()}: {PAR_WORD[status]}] " + "; ".join(msgs))
+        return f"{PAR_WORD[worst]} (worst of {world} ranks): " + " ".join(allm)
     return f"{PAR_WORD[worst]}: " + "; ".join(msgs)
 
 

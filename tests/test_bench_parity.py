@@ -67,3 +67,43 @@ def test_committed_multirank_folds_present():
             sh = D.weak_shard(r, w, 16 * bench.M)
             assert bench.golden_shard_fold(f, "cfg4", sh)[0] is not None
             assert bench.golden_shard_fold(f, "cfg2", sh)[0] is not None
+
+
+def _parity_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, ROOT)
+        import bench as B
+        from pdht_amd import dist as DD
+        # rank 0 holds a shard with a (monkeypatched) reference fold, rank 1 a shard without one
+        out = torch.arange(16, dtype=torch.int64) + rank
+        folds = {"cfg5_city64_1B_x64": {"chunk_keys": 16, "chunks": [f"{DD.fold_tensor(out, 0):016x}"]}}
+        B.golden_folds = lambda: folds
+        sh = DD.Shard(rank, world, 0 if rank == 0 else 1000, 16)
+        q.put((rank, B.check_parity(None, torch, DD, "cfg2", sh, out, None, None)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_one_unchecked_shard_makes_the_line_unchecked():
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_parity_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert got[r].startswith("unchecked (worst of 2 ranks): "), got[r]
+        assert "[rank 0: ok]" in got[r] and "[rank 1: unchecked]" in got[r]
