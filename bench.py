@@ -390,6 +390,27 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / a.steps
     elapsed_max, kern_ms_max = D.allreduce_max([elapsed, kern_ms], device=cdev)
 
+    # cfg1's step is the bound C call; the Python mirror's place_batch (its
+    # checks and pointer lookups on every call) timed the same way beside it
+    wrapper = None
+    if cfg == "cfg1":
+        wstep = lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)  # noqa: E731
+        for _ in range(a.warmup):
+            wstep()
+        w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0w = time.perf_counter()
+        w0.record()
+        for _ in range(a.steps):
+            wstep()
+        w1.record()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0w) / a.steps
+        wms = w0.elapsed_time(w1) / a.steps
+        wrapper = {"path": "pdht_amd.place_batch (Python wrapper, checks per call)",
+                   "event_ms_per_step": round(wms, 4), "wall_ms_per_step": round(wall * 1e3, 4),
+                   "Gkeys_s": round(n / max(wall, wms / 1e3) / 1e9, 4)}
+
     # -------------------------------------------- achievable read stream ---
     calib = None
     if keys is not None:
@@ -481,6 +502,8 @@ def main():
                      "calibrated_key_stream_GBps": calib_key},
         "parity": parity,
     }
+    if wrapper is not None:
+        res["cfg1_wrapper_path"] = wrapper
     if world > 1:
         res["per_rank"] = D.per_rank_report(rank, local, world, n, bytes_per_key, kern_ms, elapsed, a.steps,
                                             PEAK_HBM_GBPS, device=dev)

@@ -733,7 +733,11 @@ void k_bucket_scatter_staged(
 // Both passes take their positions from the single pass's per-tile counts
 // (count kernel + scans): no extra counting and no inter-workgroup waits.
 constexpr u32 kTpCountTile = 4096;  // counting tile = pass-1 unit
-constexpr u32 kTpMaxDigits = 256;  // F, C <= 256 (nranks <= 8192 = 2^13: product F = 2^7, C = 2^6)
+// F, C <= 256.  nranks <= 8192 = 2^13: the balanced split gives F = 2^7,
+// C = 2^6; the fine-plus split of 8/16-B array outputs (late r03,
+// pdht_bucket.hip) F = 2^8 -- at this bound -- and C = 2^5.  The launcher
+// checks both before any two-pass launch.
+constexpr u32 kTpMaxDigits = 256;
 constexpr u32 kTpChunkTiles = 8;  // counting tiles per count-chunk (one count workgroup)
 struct TwoPass {
   u32 fbits, F, C, cbits;

@@ -740,6 +740,124 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
   sink.flush();
 }
 
+// ------------------------------------------------ pipelined window kernel ---
+// Offset-indexed keys with 64-bit digests, one LDS window per wave as in
+// k_window, but with every memory latency except the window DMA's taken off a
+// tile's critical path.  k_window's tile is a chain of four dependent memory
+// round trips -- offsets (a vmcnt(0) wait that also waits for the previous
+// tile's digest store to be acknowledged), two scalar loads of the window
+// bounds, then the DMA.  Here:
+//   * the offsets of the wave's next tile are loaded while this tile's window
+//     streams in: one dwordx4 per lane = offsets[i], offsets[i+1] (index
+//     clamped to n-1, so the load is always issued and the clamped lanes read
+//     offsets[n]); the window is [lane 0's start, lane 63's end) by readlane --
+//     no scalar loads, whose lgkmcnt wait would meet the LDS reads;
+//   * a tile's digests are stored one tile late, right after the next tile's
+//     DMA and offsets load are issued, as a raw buffer store whose range
+//     check drops the lanes past n (always issued, even with no valid lane);
+//   * so the wait for a window is s_waitcnt vmcnt(2): on gfx950 loads, stores
+//     and LDS-DMA count together in issue order (MI355X_MICROARCH.md,
+//     "s_waitcnt vmcnt(N)"), and the two youngest operations are exactly that
+//     offsets load and that store -- the wait never includes a store.
+// G = tiles a wave takes in a row before jumping by the grid (1: the grid
+// stride of k_window; 16: r02's grouped order, consecutive windows per wave).
+template <int WIN, int G, class Algo, int AUX = 2>
+__global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restrict__ bytes,
+                                                        const u64 *__restrict__ offsets, u64 obase, u64 n,
+                                                        Algo algo, u64 *__restrict__ out) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
+  algo_init(algo);
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *lds = win_all + wave * (WIN / 4);
+  const u64 base = (u64)(uintptr_t)bytes;
+  // tile order: runs of G consecutive tiles, run r of wave w = gw + r * nwaves
+  const u64 gw = (u64)blockIdx.x * kWavesPerBlock + wave;
+  auto next = [&](u64 t) -> u64 {
+    if (G > 1 && (t + 1) % G != 0) return t + 1;
+    return (t / G + nwaves) * G;
+  };
+  u64 t = gw * G;
+  if (t >= ntiles) return;
+  // key i's bounds: offsets[min(i, n-1)] and the next entry (n >= 1 here)
+  auto bounds = [&](u64 tt, u64 &a, u64 &e) {
+    const u64 *p = offsets + ((tt << 6) + lane < n ? (tt << 6) + lane : n - 1);
+    a = p[0];
+    e = p[1];
+  };
+  auto rd64 = [](u64 v, u32 l) -> u64 {
+    return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) |
+           ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+  };
+  u64 a, e;
+  bounds(t, a, e);
+  u64 hprev = 0, tprev = ~0ull;  // digest of the previous tile (none yet)
+  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+  while (true) {
+    const u64 k0 = t << 6;
+    const u64 i = k0 + lane;
+    const bool valid = i < n;
+    const u64 start = a - obase;
+    const u64 end = e - obase;
+    const u64 first = rd64(a, 0) - obase;
+    const u64 whi = rd64(e, 63) - obase;
+    const u64 wlo = (base + first) & ~(u64)15;  // absolute, as in k_window
+    const u64 span = whi > first ? base + whi - wlo : 0;
+    const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)wlo);
+#pragma unroll
+    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
+      if ((u32)j * 1024 < wbytes) {  // wave-uniform
+        if ((u32)j * 1024 + lane * 16 < wbytes)
+          __builtin_amdgcn_global_load_lds(
+              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+              (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, AUX);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the next tile's offsets (always issued: clamped index; past the end the
+    // loop stops before they are used)
+    const u64 tn = next(t);
+    u64 an, en;
+    bounds(tn, an, en);
+    __builtin_amdgcn_sched_barrier(0);
+    // the previous tile's digests (always issued; records past n dropped)
+    {
+      const u64 pk = tprev << 6;
+      const u32 nrec = tprev == ~0ull ? 0u : (u32)((n - pk < 64 ? n - pk : 64) * 8);
+      __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + (tprev == ~0ull ? 0 : pk), 0, nrec,
+                                                                   0x00020000);
+      const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, AUX);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+      const u64 len = end - start;
+      if (base + end - wlo <= wbytes)
+        hprev = algo(LdsReader{lds, (u32)(base + start - wlo)}, len);
+      else
+        hprev = algo(GlobalReader{bytes + start}, len);
+    }
+    tprev = t;
+    __builtin_amdgcn_wave_barrier();  // window reused by the next tile
+    if (tn >= ntiles) break;
+    t = tn;
+    a = an;
+    e = en;
+  }
+  // the last tile's digests
+  const u64 pk = tprev << 6;
+  const u32 nrec = (u32)((n - pk < 64 ? n - pk : 64) * 8);
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + pk, 0, nrec, 0x00020000);
+  const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, AUX);
+}
+
 // ---------------------------------------------------------- long keys ---
 // Keys far longer than a 64-key LDS window can hold (fixed L > 255 B): each
 // lane walks its own key straight from global memory (GlobalReader); the

@@ -302,6 +302,27 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
 #ifdef PDHT_HIP_TUNING
   if (tuning_variant() == 12) wide = false;
   if (tuning_variant() == 13) wide = true;
+  if constexpr (std::is_same<Algo, AlgoCity64>::value && std::is_same<Sink, Sink64>::value) {
+    const int v = tuning_variant();
+    if (v >= 170 && v <= 173) {  // pipelined window kernel (offsets a tile ahead, stores a tile late)
+      const int pc = v == 173 ? 3 : 4;
+      if (v == 170 || v == 173) {
+        g_kernel = v == 170 ? "k_window_pipe<var,10224,G1>@4" : "k_window_pipe<var,10224,G1>@3";
+        k_window_pipe<10224, 1, Algo, 2><<<grid_for(wb, pc, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                     sink.out);
+      } else if (v == 171) {
+        g_kernel = "k_window_pipe<var,10224,G4>@4";
+        k_window_pipe<10224, 4, Algo, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                    sink.out);
+      } else {
+        g_kernel = "k_window_pipe<var,10224,G16>@4";
+        k_window_pipe<10224, 16, Algo, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
+                                                                                     sink.out);
+      }
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+  }
 #endif
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";

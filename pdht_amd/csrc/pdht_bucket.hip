@@ -278,6 +278,10 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     tp.F = 1u << tp.fbits;
     tp.C = (nranks + tp.F - 1) >> tp.fbits;
     tp.cbits = a.nbits - tp.fbits;
+    static_assert(kBucketMaxRanks <= kTpMaxDigits * kTpMaxDigits, "two digits of <= 256 cover every rank");
+    if (tp.F > kTpMaxDigits || tp.C > kTpMaxDigits)  // the kernels' LDS digit tables
+      return fail("two-pass digit split: a digit of %s%lld buckets exceeds the LDS tables", "",
+                  (long long)(tp.F > kTpMaxDigits ? tp.F : tp.C));
     tp.countsF = w.countsF;
     tp.chunksF = w.chunksF;
     tp.totalsF = w.totalsF;

@@ -22,6 +22,9 @@ extern "C" {
  *                153  timing only: CRC lookups replaced by a fold (wrong digests)
  *                150  CRC-32C on r02's 6-bit-slice tables (product: byte tables)
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
+ *            170-173  CityHash64: k_window_pipe (offsets a tile ahead, digests a tile
+ *                     late, vmcnt(2)): G = 1 / 4 / 16 consecutive tiles per wave at
+ *                     4 WG/CU; 173 = G 1 at 3 WG/CU
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,
  *                     41 default-policy DMA, 42 plain stores, 43 3 WG/CU,

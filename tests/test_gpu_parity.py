@@ -278,7 +278,9 @@ def test_var_golden_mixed(dev, golden, oracle):
     assert (u64(P.citycrc128_var_batch(dd, od)) == golden["mixed_city128"]).all()
 
 
-VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2"}
+VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2",
+               170: "k_window_pipe<var,10224,G1>@4", 171: "k_window_pipe<var,10224,G4>@4",
+               172: "k_window_pipe<var,10224,G16>@4", 173: "k_window_pipe<var,10224,G1>@3"}
 
 
 def auto_var_kernel(total_bytes, n):
@@ -484,6 +486,10 @@ def test_device_wrappers_validate_outputs(dev):
 
 BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1000, 4096, 4097, 8192)
                 for n in (0, 1, 4095, 100003)]
+# the product's two-pass entry points with the fine-plus digit split:
+# 8-B keys from 1536 ranks (nbits 11: F = 128, C = 12 at 1536), 16-B keys from 1025
+BUCKET_CASES += [(L, nr, n, 0) for (L, nr) in ((8, 1536), (8, 2047), (16, 1025), (16, 2048))
+                 for n in (4095, 300007)]
 BUCKET_CASES += [(L, nr, n, 21) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192) for n in (4095, 300007)]
 BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2048, 2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]

@@ -5,7 +5,8 @@ stream; every variant's output is compared with the product kernel's.
 
   python tools/abbench.py --work cfg2 --variants 0,7,26 [--per-cu 0,2,3,4]
   works: cfg2 (16M x 64 B City64), cfg4 (Crc128), cfg3 (64M mixed 16..256 B),
-         cfg3c (64M x 136 B through the variable-length path), cfg3fold (cfg3's
+         cfg3c (64M x 136 B through the variable-length path), cfg3s<G> / cfg3sall
+         (cfg3 with the lengths sorted inside groups of G keys / overall), cfg3fold (cfg3's
          window data movement: fold of the bytes; variant 40 = no LDS reads),
          varfold_<L> (64M x L-B fixed keys through the var calibration entry),
          long (1M x 1 KiB Crc128), long64 (1M x 1 KiB City64),
@@ -112,11 +113,17 @@ def workload(name, dev):
         offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device=dev)
         out = torch.empty(n, dtype=torch.int64, device=dev)
         return (lambda: P.key_stream_var(data, offs, out=out, check=False)), (lambda: out[:1].clone()), n * (L + 16)
-    if name not in ("cfg3", "cfg3c", "cfg3fold", "cfg3cfold"):
+    if name not in ("cfg3", "cfg3c", "cfg3fold", "cfg3cfold", "cfg3s128", "cfg3s256", "cfg3s1024", "cfg3sall"):
         raise SystemExit(f"unknown work {name}")
     n = 64 * M
     lo, hi = (136, 136) if name in ("cfg3c", "cfg3cfold") else (16, 256)
     lens = P.mixed_lengths(0x1E575EED1E575EED, 0, n, lo, hi, device=dev)
+    if name.startswith("cfg3s"):
+        # cfg3's lengths sorted inside every group of G keys (sall: all of them):
+        # the same bytes, but each 64-key tile holds keys of similar length --
+        # what regrouping keys by length class across G/64 waves could buy
+        g = n if name == "cfg3sall" else int(name[5:])
+        lens = lens.view(-1, g).sort(dim=1).values.reshape(-1)
     offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     torch.cumsum(lens, 0, out=offs[1:])
     total = int(offs[-1].item())
