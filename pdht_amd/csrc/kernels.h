@@ -67,6 +67,44 @@ struct LdsReader {
   }
 };
 
+// The same spans as UNALIGNED LDS loads: gfx950 serves ds_read_b128 /
+// ds_read_b64 / ds_read_b32 at any byte address (HSA runs with unaligned
+// access mode; hipcc emits them for under-aligned LDS types on its own), so a
+// span needs no v_alignbyte_b32 at all -- 64 B = 4 ds_read_b128 instead of 9
+// ds_read2_b32 + 16 VALU funnel shifts.
+struct LdsReaderU {
+  const u32 *lds;
+  u32 base;
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> span(u32 o) const {
+    typedef u32x4 u32x4u __attribute__((aligned(1)));
+    typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+    typedef u32x2 u32x2u __attribute__((aligned(1)));
+    typedef u32 u32u __attribute__((aligned(1)));
+    const uint8_t *p = reinterpret_cast<const uint8_t *>(lds) + base + o;
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 16; ++j) {
+      const u32x4 v = *reinterpret_cast<const u32x4u *>(p + 16 * j);
+      w.d[4 * j + 0] = v.x;
+      w.d[4 * j + 1] = v.y;
+      w.d[4 * j + 2] = v.z;
+      w.d[4 * j + 3] = v.w;
+    }
+    if constexpr (N % 16 >= 8) {
+      const u32x2 v = *reinterpret_cast<const u32x2u *>(p + N / 16 * 16);
+      w.d[N / 16 * 4] = v.x;
+      w.d[N / 16 * 4 + 1] = v.y;
+    }
+    if constexpr (N % 8 == 4) w.d[N / 4 - 1] = *reinterpret_cast<const u32u *>(p + N - 4);
+    return w;
+  }
+  __device__ __forceinline__ u32 w32(u32 o) const { return span<4>(o).d[0]; }
+  __device__ __forceinline__ u32 b8(u32 o) const {
+    return reinterpret_cast<const uint8_t *>(lds)[base + o];
+  }
+};
+
 // Key bytes straight from global memory (keys outside the LDS window): the
 // same dword-run + funnel shape on the dword-aligned address.  The extra
 // trailing dword is only read when the span is misaligned (it then holds key
@@ -659,7 +697,7 @@ __global__ __launch_bounds__(BLOCK) void k_fixed_xpose64(const uint8_t *__restri
 // Any key length.  VAR: key i = bytes[offsets[i]-obase, offsets[i+1]-obase);
 // otherwise key i = bytes[i*stride, i*stride+keylen).  WIN = LDS bytes per
 // wave.  AUX = cache-policy bits of the LDS-DMA (2 = non-temporal).
-template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0, int ALIGN = 16>
+template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0, int ALIGN = 16, class LR = LdsReader>
 __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -730,7 +768,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
       const u64 len = end - start;
       typename Algo::Out h;
       if (base + end - wlo <= wbytes)
-        h = algo(LdsReader{lds, (u32)(base + start - wlo)}, len);
+        h = algo(LR{lds, (u32)(base + start - wlo)}, len);
       else
         h = algo(GlobalReader{bytes + start}, len);
       sink.put(i, h);
@@ -761,7 +799,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
 //     offsets load and that store -- the wait never includes a store.
 // G = tiles a wave takes in a row before jumping by the grid (1: the grid
 // stride of k_window; 16: r02's grouped order, consecutive windows per wave).
-template <int WIN, int G, class Algo, int AUX = 2>
+template <int WIN, int G, class Algo, int AUX = 2, class LR = LdsReader>
 __global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restrict__ bytes,
                                                         const u64 *__restrict__ offsets, u64 obase, u64 n,
                                                         Algo algo, u64 *__restrict__ out) {
@@ -839,7 +877,7 @@ __global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restric
     if (valid) {
       const u64 len = end - start;
       if (base + end - wlo <= wbytes)
-        hprev = algo(LdsReader{lds, (u32)(base + start - wlo)}, len);
+        hprev = algo(LR{lds, (u32)(base + start - wlo)}, len);
       else
         hprev = algo(GlobalReader{bytes + start}, len);
     }

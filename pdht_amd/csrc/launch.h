@@ -304,6 +304,19 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
   if (tuning_variant() == 13) wide = true;
   if constexpr (std::is_same<Algo, AlgoCity64>::value && std::is_same<Sink, Sink64>::value) {
     const int v = tuning_variant();
+    if (v == 174 || v == 175) {  // unaligned ds_read_b128 spans (no v_alignbyte_b32)
+      if (v == 174) {
+        g_kernel = "k_window_pipe<var,10224,G1,lds-u>@4";
+        k_window_pipe<10224, 1, Algo, 2, LdsReaderU><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+            b, offsets, obase, n, algo, sink.out);
+      } else {
+        g_kernel = "k_window<var,nt,10224,lds-u>@4";
+        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReaderU><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
+      }
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
     if (v >= 170 && v <= 173) {  // pipelined window kernel (offsets a tile ahead, stores a tile late)
       const int pc = v == 173 ? 3 : 4;
       if (v == 170 || v == 173) {

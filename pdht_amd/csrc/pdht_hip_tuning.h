@@ -24,7 +24,8 @@ extern "C" {
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
  *            170-173  CityHash64: k_window_pipe (offsets a tile ahead, digests a tile
  *                     late, vmcnt(2)): G = 1 / 4 / 16 consecutive tiles per wave at
- *                     4 WG/CU; 173 = G 1 at 3 WG/CU
+ *                     4 WG/CU; 173 = G 1 at 3 WG/CU; 174 = G 1 with unaligned
+ *                     ds_read_b128 spans (LdsReaderU); 175 = k_window with them
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,
  *                     41 default-policy DMA, 42 plain stores, 43 3 WG/CU,

@@ -280,7 +280,8 @@ def test_var_golden_mixed(dev, golden, oracle):
 
 VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2",
                170: "k_window_pipe<var,10224,G1>@4", 171: "k_window_pipe<var,10224,G4>@4",
-               172: "k_window_pipe<var,10224,G16>@4", 173: "k_window_pipe<var,10224,G1>@3"}
+               172: "k_window_pipe<var,10224,G16>@4", 173: "k_window_pipe<var,10224,G1>@3",
+               174: "k_window_pipe<var,10224,G1,lds-u>@4", 175: "k_window<var,nt,10224,lds-u>@4"}
 
 
 def auto_var_kernel(total_bytes, n):
