@@ -10,8 +10,9 @@
 //   * HostReader    -- the scalar host API (memcpy)              city_host.hip
 //   * RegReader<W>  -- fixed-length keys already in VGPRs; with a constant
 //                      length every window folds to register renaming
-//   * LdsReader     -- keys in an LDS window at arbitrary byte offsets: one
-//                      run of dword reads + v_alignbyte_b32 per window
+//   * LdsReader     -- keys in an LDS window at arbitrary byte offsets:
+//                      unaligned ds_read_b128/b64/b32 per window (r04; the
+//                      r01-r03 dword runs + v_alignbyte_b32 are LdsReaderFunnel)
 //   * GlobalReader  -- the same straight from global memory (keys that do not
 //                      fit the LDS window)
 // Behaviour follows /root/reference/libpdht/city.c; each routine cites the

@@ -12,9 +12,8 @@
 //     lane holds its own key in VGPRs;
 //   * k_window: any key length, fixed stride or offset-indexed: the wave's
 //     contiguous byte range is DMA'd into a per-wave LDS window and each lane
-//     hashes its key out of LDS with byte-aligned fetches
-//     (v_alignbyte_b32); keys that do not fit the window are read from
-//     global memory directly;
+//     hashes its key out of LDS with unaligned ds_read_b128 spans; keys that
+//     do not fit the window are read from global memory directly;
 //   * k_global: fixed keys too long for a 64-key window, each lane walking
 //     its own key in global memory.
 // All kernels are grid-stride persistent loops (grid ~ CUs x residency) and
@@ -40,11 +39,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // --------------------------------------------------------------- readers ---
-// Key bytes in LDS at an arbitrary byte offset.  A span of N bytes is one run
-// of N/4+1 dword reads from one base address (ds_read2_b32 with immediate
-// offsets, a single wait) funnelled by v_alignbyte_b32; the window carries
-// 16 B of slack so the trailing dword read stays in the array.
-struct LdsReader {
+// Key bytes in LDS at an arbitrary byte offset, r01-r03 form (tuning variant
+// 175 now): a span of N bytes is one run of N/4+1 dword reads from one base
+// address (ds_read2_b32 with immediate offsets, a single wait) funnelled by
+// v_alignbyte_b32; the window carries 16 B of slack so the trailing dword
+// read stays in the array.
+struct LdsReaderFunnel {
   const u32 *lds;
   u32 base;
   template <int N>
@@ -67,12 +67,15 @@ struct LdsReader {
   }
 };
 
-// The same spans as UNALIGNED LDS loads: gfx950 serves ds_read_b128 /
-// ds_read_b64 / ds_read_b32 at any byte address (HSA runs with unaligned
-// access mode; hipcc emits them for under-aligned LDS types on its own), so a
-// span needs no v_alignbyte_b32 at all -- 64 B = 4 ds_read_b128 instead of 9
-// ds_read2_b32 + 16 VALU funnel shifts.
-struct LdsReaderU {
+// Key bytes in LDS at an arbitrary byte offset (product, r04): spans as
+// UNALIGNED LDS loads.  gfx950 serves ds_read_b128 / ds_read_b64 /
+// ds_read_b32 at any byte address (HSA runs with unaligned access mode;
+// hipcc emits them for under-aligned LDS types on its own), so a span needs
+// no v_alignbyte_b32 at all -- 64 B = 4 ds_read_b128 instead of 9
+// ds_read2_b32 + 16 VALU funnel shifts (window kernel: static VALU 1145 ->
+// 1030; cfg3 +2.5 / +2.8 % on two boxes, interleaved, profiles/r04/ab/).
+// Reads stay inside the key's bytes.
+struct LdsReader {
   const u32 *lds;
   u32 base;
   template <int N>
@@ -799,7 +802,10 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
 //     offsets load and that store -- the wait never includes a store.
 // G = tiles a wave takes in a row before jumping by the grid (1: the grid
 // stride of k_window; 16: r02's grouped order, consecutive windows per wave).
-template <int WIN, int G, class Algo, int AUX = 2, class LR = LdsReader>
+// RING (calibration only): digests of tile t go to out + 64 * (t % RING), an
+// L2-resident destination -- the kernel without its HBM writes.
+// SAUX: cache-policy bits of the digest stores (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
+template <int WIN, int G, class Algo, int AUX = 2, class LR = LdsReader, u64 RING = 0, int SAUX = AUX>
 __global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restrict__ bytes,
                                                         const u64 *__restrict__ offsets, u64 obase, u64 n,
                                                         Algo algo, u64 *__restrict__ out) {
@@ -866,10 +872,10 @@ __global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restric
     {
       const u64 pk = tprev << 6;
       const u32 nrec = tprev == ~0ull ? 0u : (u32)((n - pk < 64 ? n - pk : 64) * 8);
-      __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + (tprev == ~0ull ? 0 : pk), 0, nrec,
-                                                                   0x00020000);
+      const u64 dst = tprev == ~0ull ? 0 : RING ? (tprev % RING) << 6 : pk;
+      __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + dst, 0, nrec, 0x00020000);
       const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
-      __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
     }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -891,9 +897,10 @@ __global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restric
   // the last tile's digests
   const u64 pk = tprev << 6;
   const u32 nrec = (u32)((n - pk < 64 ? n - pk : 64) * 8);
-  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + pk, 0, nrec, 0x00020000);
+  __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(out + (RING ? (tprev % RING) << 6 : pk), 0, nrec, 0x00020000);
   const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
 }
 
 // ---------------------------------------------------------- long keys ---

@@ -304,15 +304,34 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
   if (tuning_variant() == 13) wide = true;
   if constexpr (std::is_same<Algo, AlgoCity64>::value && std::is_same<Sink, Sink64>::value) {
     const int v = tuning_variant();
-    if (v == 174 || v == 175) {  // unaligned ds_read_b128 spans (no v_alignbyte_b32)
+    if (v >= 180 && v <= 187) {  // cache policies of the pipe kernel's DMA / digest stores
+      auto go = [&](auto kern, const char *tag) {
+        g_kernel = tag;
+        kern<<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo, sink.out);
+      };
+      switch (v) {
+        case 180: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 0>, "k_window_pipe<dma nt,st plain>"); break;
+        case 181: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 1>, "k_window_pipe<dma nt,st sc0>"); break;
+        case 182: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 16>, "k_window_pipe<dma nt,st sc1>"); break;
+        case 183: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 18>, "k_window_pipe<dma nt,st sc1 nt>"); break;
+        case 184: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 19>, "k_window_pipe<dma nt,st sc0 sc1 nt>"); break;
+        case 185: go(k_window_pipe<10224, 1, Algo, 0, LdsReader, 0, 2>, "k_window_pipe<dma plain,st nt>"); break;
+        case 186: go(k_window_pipe<10224, 1, Algo, 3, LdsReader, 0, 2>, "k_window_pipe<dma sc0 nt,st nt>"); break;
+        default: go(k_window_pipe<10224, 1, Algo, 16, LdsReader, 0, 2>, "k_window_pipe<dma sc1,st nt>"); break;
+      }
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+    if (v == 174 || v == 175) {  // 174: pipe kernel, r03 funnel reader; 175: product kernel, r03 reader
       if (v == 174) {
-        g_kernel = "k_window_pipe<var,10224,G1,lds-u>@4";
-        k_window_pipe<10224, 1, Algo, 2, LdsReaderU><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+        g_kernel = "k_window_pipe<var,10224,G1,funnel>@4";
+        k_window_pipe<10224, 1, Algo, 2, LdsReaderFunnel><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
             b, offsets, obase, n, algo, sink.out);
       } else {
-        g_kernel = "k_window<var,nt,10224,lds-u>@4";
-        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReaderU><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
+        g_kernel = "k_window<var,nt,10224,funnel>@4";
+        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReaderFunnel>
+            <<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n, algo,
+                                                     Sink64T<true>{nullptr, sink.out});
       }
       HIP_TRY(hipGetLastError());
       return 0;

@@ -24,14 +24,20 @@ extern "C" {
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
  *            170-173  CityHash64: k_window_pipe (offsets a tile ahead, digests a tile
  *                     late, vmcnt(2)): G = 1 / 4 / 16 consecutive tiles per wave at
- *                     4 WG/CU; 173 = G 1 at 3 WG/CU; 174 = G 1 with unaligned
- *                     ds_read_b128 spans (LdsReaderU); 175 = k_window with them
+ *                     4 WG/CU; 173 = G 1 at 3 WG/CU; 174 = G 1 / 175 = the product
+ *                     window kernel with the r03 funnel reader (dword runs +
+ *                     v_alignbyte_b32; product since r04: unaligned ds_read_b128)
  *   calibration 40-45 (pdht_hip_key_stream_var_dev) the window kernel's data
  *                     movement alone (digest = key length): 40 as shipped,
  *                     41 default-policy DMA, 42 plain stores, 43 3 WG/CU,
  *                     44/45 windows on 128-B lines
  *           110 / 111 (same entry) the window kernel hashing every key twice
  *                     / once: what the arithmetic costs over 40
+ *            180-187  k_window_pipe G1 cache policies (DMA / digest stores): nt / plain,
+ *                     nt / sc0, nt / sc1, nt / sc1|nt, nt / sc0|sc1|nt, plain / nt,
+ *                     sc0|nt / nt, sc1 / nt
+ *            176-179  (same entry) k_window_pipe: length-only with stores / into a
+ *                     32 KiB ring; CityHash64 with stores / into the ring
  *       119-121, 125  (same entry) keys read as fixed rows of the mean length,
  *                     no offsets: nt / no / plain digest stores / plain stores
  *                     into 32 KiB (L2-resident)

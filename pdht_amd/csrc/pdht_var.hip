@@ -105,6 +105,31 @@ PDHT_API int pdht_hip_key_stream_var_dev(const void *bytes, size_t nbytes, const
     HIP_TRY(hipGetLastError());
     return 0;
   }
+  if (v >= 176 && v <= 179) {
+    // the pipelined window kernel's data movement (digest = key length, no
+    // LDS reads): 176 with its stores, 177 stores into a 32 KiB ring (no HBM
+    // writes); 178/179 the same with CityHash64 (178 = variant 170's kernel)
+    if (n == 0) return 0;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    const uint8_t *b = static_cast<const uint8_t *>(bytes);
+    const u64 wb = ((n + 63) / 64 + 3) / 4;
+    g_kernel = "k_window_pipe<var,calib>";
+    if (v == 176)
+      k_window_pipe<10224, 1, AlgoLenOnly, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(b, offsets, 0, n,
+                                                                                          AlgoLenOnly{}, out);
+    else if (v == 177)
+      k_window_pipe<10224, 1, AlgoLenOnly, 2, LdsReader, 64><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
+          b, offsets, 0, n, AlgoLenOnly{}, out);
+    else if (v == 178)
+      k_window_pipe<10224, 1, AlgoCity64, 2><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(b, offsets, 0, n,
+                                                                                         AlgoCity64{}, out);
+    else
+      k_window_pipe<10224, 1, AlgoCity64, 2, LdsReader, 64><<<grid_for(wb, 4, dev), kBlock, 0, ST(s)>>>(
+          b, offsets, 0, n, AlgoCity64{}, out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   if (v >= 40 && v <= 45) {
     if (n == 0) return 0;
     int dev;
