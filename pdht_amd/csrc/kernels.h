@@ -435,6 +435,35 @@ struct Sink128T {
   __host__ Sink128T shift(u64 k0) const { return Sink128T{lds_hist, out + 2 * k0}; }
 };
 typedef Sink64T<false> Sink64;
+
+// 64-bit digests stored 16 B per lane: every even lane takes its odd
+// neighbour's digest (two DPP row_shl:1 moves) and stores both with one
+// dwordx4, so a wave's 512 B of digests leave as 32 lane-stores instead of
+// 64 (i must be 64-aligned tile base + lane, as in every kernel here; a lane
+// whose partner is inactive -- past the batch's end, or in another branch of
+// a divergent hash -- stores its own digest alone).
+template <bool NTS = true>
+struct Sink64x2T {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64 i, u64 h) {
+    const u32 lo = (u32)h, hi = (u32)(h >> 32);
+    const u32 lo1 = __builtin_amdgcn_mov_dpp(lo, 0x101, 0xf, 0xf, false);  // row_shl:1: lane l <- l+1
+    const u32 hi1 = __builtin_amdgcn_mov_dpp(hi, 0x101, 0xf, 0xf, false);
+    const u32 lane = (u32)i & 63;
+    // partner = the other lane of the pair; the two may sit in different
+    // divergent branches (then each stores its own digest)
+    const bool partner = (__builtin_amdgcn_read_exec() >> (lane ^ 1)) & 1;
+    if ((lane & 1) == 0 && partner)
+      st<NTS>(u32x4{lo, hi, lo1, hi1}, reinterpret_cast<u32x4 *>(out + i));
+    else if (!partner)
+      st<NTS>(h, out + i);
+  }
+  __device__ __forceinline__ void flush() {}
+  __host__ Sink64x2T shift(u64 k0) const { return Sink64x2T{lds_hist, out + k0}; }
+};
 typedef Sink128T<false> Sink128;
 
 #ifdef PDHT_HIP_TUNING

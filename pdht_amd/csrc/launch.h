@@ -165,6 +165,15 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
         HIP_TRY(hipGetLastError());
         return 0;
       }
+      if constexpr (std::is_same<Sink, Sink64>::value) {
+        if (tuning_variant() == 188) {  // digests stored 16 B per lane (even lanes, DPP pairs)
+          g_kernel = "k_fixed_xpose64<nt,d2,st16>@3";
+          k_fixed_xpose64<Algo, Sink64x2T<true>, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+              k, n, algo, Sink64x2T<true>{nullptr, sink.out});
+          HIP_TRY(hipGetLastError());
+          return 0;
+        }
+      }
       if (tuning_variant() == 26) {  // plain digest stores (r01: 2-6 % slower)
         g_kernel = "k_fixed_xpose64<nt-load,plain-store,d2>@3";
         k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
@@ -319,6 +328,13 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
         case 186: go(k_window_pipe<10224, 1, Algo, 3, LdsReader, 0, 2>, "k_window_pipe<dma sc0 nt,st nt>"); break;
         default: go(k_window_pipe<10224, 1, Algo, 16, LdsReader, 0, 2>, "k_window_pipe<dma sc1,st nt>"); break;
       }
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+    if (v == 189) {  // the product window kernel, digests stored 16 B per lane
+      g_kernel = "k_window<var,nt,10224,st16>@4";
+      k_window<10224, true, Algo, Sink64x2T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+          b, offsets, obase, 0, 0, n, algo, Sink64x2T<true>{nullptr, sink.out});
       HIP_TRY(hipGetLastError());
       return 0;
     }

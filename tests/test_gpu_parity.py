@@ -167,7 +167,7 @@ def _variants(vs):
     return [v if v == 0 else pytest.param(v, marks=pytest.mark.tuning) for v in vs]
 
 
-VARIANT_KERNELS = {0: "k_fixed_xpose64<nt,d2>@3", 7: "k_fixed_xpose64<nt,d1>@4",
+VARIANT_KERNELS = {0: "k_fixed_xpose64<nt,d2>@3", 7: "k_fixed_xpose64<nt,d1>@4", 188: "k_fixed_xpose64<nt,d2,st16>@3",
                    26: "k_fixed_xpose64<nt-load,plain-store,d2>@3"}
 
 
@@ -281,7 +281,8 @@ def test_var_golden_mixed(dev, golden, oracle):
 VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,16K>@2",
                170: "k_window_pipe<var,10224,G1>@4", 171: "k_window_pipe<var,10224,G4>@4",
                172: "k_window_pipe<var,10224,G16>@4", 173: "k_window_pipe<var,10224,G1>@3",
-               174: "k_window_pipe<var,10224,G1,funnel>@4", 175: "k_window<var,nt,10224,funnel>@4"}
+               174: "k_window_pipe<var,10224,G1,funnel>@4", 175: "k_window<var,nt,10224,funnel>@4",
+               189: "k_window<var,nt,10224,st16>@4"}
 
 
 def auto_var_kernel(total_bytes, n):
