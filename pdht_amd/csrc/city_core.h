@@ -23,6 +23,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <utility>
+
 #define PDHT_HD __host__ __device__ __forceinline__
 
 namespace pdht {
@@ -561,29 +563,23 @@ PDHT_HD void crc_block_lines_ph(const R &s, u32 o, u32 ph, Words<28> &carry, Wor
   }
 }
 
-template <class R, class Tab = CrcConstTab>
-PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T = Tab{}) {
-  // line form: block k ends at or before its line-aligned load end B(k) =
-  // 240k + 16(k mod 8) + 256 (or + 128); while B <= len the blocks stream as
-  // whole lines, after that (only near the key's end) as plain 240-B spans
-  Words<60> q;
-  Words<28> carry;
-  constexpr bool kLn = ReaderLines<R>::value;
-  auto line_end = [](u64 k) { return 240 * k + 16 * (k & 7) + ((k & 7) == 7 ? 128 : 256); };
-  if (kLn && line_end(0) <= len)
-    crc_block_lines<0>(s, 0, carry, q);
-  else
-    q = s.template span<240>(0);  // block 0 (len >= 240)
-  u64 a = q.w64(56) + kK0;
-  u64 b = q.w64(96) + kK0;
-  u64 c = out[0] = mix16(b, len);
-  u64 d = out[1] = q.w64(120) * kK0 + len;
-  u64 e = q.w64(184) + seed;
-  u64 f = seed, g = 0, h = 0, i = 0, j = 0;
-  u64 t = c + d;
-  u32 o = 0;
-  // one 40-byte CHUNK (city.c:425-440) over the words w0..w4
-  auto chunk = [&](u64 w0, u64 w1, u64 w2, u64 w3, u64 w4, u64 mult, u32 flip) {
+// Readers that set kStream run CityHashCrc256Long's block loop as a stream of
+// 128-B lines (crc256_stream below).
+template <class R, class = void>
+struct ReaderStream {
+  static constexpr bool value = false;
+};
+template <class R>
+struct ReaderStream<R, decltype((void)R::kStream)> {
+  static constexpr bool value = R::kStream;
+};
+
+// CityHashCrc256Long's state (city.c:412-423) and its 40-byte CHUNK
+// (city.c:425-440).
+template <class Tab>
+struct Crc256State {
+  u64 a, b, c, d, e, f, g, h, i, j, t;
+  PDHT_HD void chunk(u64 w0, u64 w1, u64 w2, u64 w3, u64 w4, u64 mult, u32 flip, const Tab &T) {
     const u64 a0 = a;
     a = rotr(b, 41u ^ flip) * mult + w0;
     b = rotr(c, 27u ^ flip) * mult + w1;
@@ -596,32 +592,135 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
     h = crc32c_u64(h, c, T);
     i = crc32c_u64(i, d, T);
     j = crc32c_u64(j, e, T);
-  };
-  auto chunk_at = [&](const Words<60> &w, u32 base, u64 mult, u32 flip) {
-    chunk(w.w64(base), w.w64(base + 8), w.w64(base + 16), w.w64(base + 24), w.w64(base + 32), mult, flip);
-  };
-  const u64 blocks = len / 240;
-  u64 rest = len - blocks * 240;
-  for (u64 k = 0; k < blocks; ++k) {
-    // (prefetching the next block as well measured equal, r02: 165 VGPRs)
-    if (k) {
-      if (kLn && line_end(k) <= len)  // uniform for fixed-length batches
-        crc_block_lines_ph(s, o, (u32)k & 7, carry, q);
+  }
+};
+
+// The block loop of CityHashCrc256Long (city.c:424-442) as a stream of whole
+// 128-B lines (r04).  The 6 * (len / 240) block chunks of 40 B are one run of
+// 8-B words over the key: chunk c = words [5c, 5c + 5), with the multiplier
+// 1 / k0 and the rotation flip alternating by chunk parity (six chunks per
+// block keep the alternation across blocks).  Lines come in two register
+// buffers, even lines in A and odd ones in B; the moment a chunk has consumed
+// the last word of line l, line l + 2 is requested into l's buffer, so one
+// line's load is always in flight behind ~3 chunks of mixing -- per lane 128-B
+// line loads (8 x dwordx4) instead of the 256-B line spans of the block form,
+// and about half its registers.  Unrolled over 32 chunks = 10 lines (the two
+// buffers' roles then repeat); chunks past the block loop are skipped
+// (uniform for fixed-length keys).  Lines are read only below len (pieces of
+// a line that start at or past len stay zero and are never used).
+template <class R, class Tab>
+struct Crc256Stream {
+  const R &s;
+  u64 len, nch, nlines;
+  Crc256State<Tab> &st;
+  const Tab &T;
+  Words<32> A, B;
+  PDHT_HD void load(u64 l, Words<32> &dst) const {
+    if (l < nlines) dst = s.template line_lim<128>((u32)(128 * l), (u32)len);
+  }
+  template <int K>
+  PDHT_HD u64 word() const {
+    constexpr int line = K / 16, at = 8 * (K % 16);
+    if constexpr (line % 2 == 0)
+      return A.w64(at);
+    else
+      return B.w64(at);
+  }
+  // chunk C (0..31) of the double period that starts at chunk c0, line l0
+  template <int C>
+  PDHT_HD void step(u64 c0, u64 l0) {
+    if (c0 + C >= nch) return;  // past the block loop (uniform)
+    constexpr int k = 5 * C;
+    st.chunk(word<k>(), word<k + 1>(), word<k + 2>(), word<k + 3>(), word<k + 4>(), (C & 1) ? kK0 : 1,
+             (C & 1) ? 0u : 1u, T);
+    constexpr int l1 = k / 16;
+    if constexpr ((k + 5) / 16 > l1) {  // line l1 fully consumed: its buffer takes line l1 + 2
+      if constexpr (l1 % 2 == 0)
+        load(l0 + l1 + 2, A);
       else
-        q = s.template span<240>(o);
+        load(l0 + l1 + 2, B);
     }
-    chunk_at(q, 0, 1, 1);
-    chunk_at(q, 40, kK0, 0);
-    chunk_at(q, 80, 1, 1);
-    chunk_at(q, 120, kK0, 0);
-    chunk_at(q, 160, 1, 1);
-    chunk_at(q, 200, kK0, 0);
-    o += 240;
+  }
+  template <int... C>
+  PDHT_HD void period(u64 c0, u64 l0, std::integer_sequence<int, C...>) {
+    (step<C>(c0, l0), ...);
+  }
+};
+
+template <class R, class Tab>
+PDHT_HD void crc256_stream_blocks(const R &s, u64 len, u32 seed, u64 out[4], Crc256State<Tab> &st,
+                                  const Tab &T) {
+  const u64 blocks = len / 240;
+  Crc256Stream<R, Tab> S{s, len, 6 * blocks, (240 * blocks + 127) / 128, st, T, {}, {}};
+  S.load(0, S.A);
+  S.load(1, S.B);
+  // block 0's opening words (city.c:414-419): bytes 56, 96, 120 (line 0), 184 (line 1)
+  st.a = S.A.w64(56) + kK0;
+  st.b = S.A.w64(96) + kK0;
+  st.c = out[0] = mix16(st.b, len);
+  st.d = out[1] = S.A.w64(120) * kK0 + len;
+  st.e = S.B.w64(56) + seed;
+  st.f = seed;
+  st.g = st.h = st.i = st.j = 0;
+  st.t = st.c + st.d;
+  for (u64 c0 = 0, l0 = 0; c0 < S.nch; c0 += 32, l0 += 10)
+    S.period(c0, l0, std::make_integer_sequence<int, 32>{});
+}
+
+template <class R, class Tab = CrcConstTab>
+PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T = Tab{}) {
+  Crc256State<Tab> st;
+  const u64 blocks = len / 240;
+  if constexpr (ReaderStream<R>::value) {
+    crc256_stream_blocks(s, len, seed, out, st, T);  // kStream readers: 128-B line stream
+  } else {
+    // line form: block k ends at or before its line-aligned load end B(k) =
+    // 240k + 16(k mod 8) + 256 (or + 128); while B <= len the blocks stream as
+    // whole lines, after that (only near the key's end) as plain 240-B spans
+    Words<60> q;
+    Words<28> carry;
+    constexpr bool kLn = ReaderLines<R>::value;
+    auto line_end = [](u64 k) { return 240 * k + 16 * (k & 7) + ((k & 7) == 7 ? 128 : 256); };
+    if (kLn && line_end(0) <= len)
+      crc_block_lines<0>(s, 0, carry, q);
+    else
+      q = s.template span<240>(0);  // block 0 (len >= 240)
+    st.a = q.w64(56) + kK0;
+    st.b = q.w64(96) + kK0;
+    st.c = out[0] = mix16(st.b, len);
+    st.d = out[1] = q.w64(120) * kK0 + len;
+    st.e = q.w64(184) + seed;
+    st.f = seed;
+    st.g = st.h = st.i = st.j = 0;
+    st.t = st.c + st.d;
+    auto chunk_at = [&](const Words<60> &w, u32 base, u64 mult, u32 flip) {
+      st.chunk(w.w64(base), w.w64(base + 8), w.w64(base + 16), w.w64(base + 24), w.w64(base + 32), mult, flip,
+               T);
+    };
+    u32 o = 0;
+    for (u64 k = 0; k < blocks; ++k) {
+      // (prefetching the next block as well measured equal, r02: 165 VGPRs)
+      if (k) {
+        if (kLn && line_end(k) <= len)  // uniform for fixed-length batches
+          crc_block_lines_ph(s, o, (u32)k & 7, carry, q);
+        else
+          q = s.template span<240>(o);
+      }
+      chunk_at(q, 0, 1, 1);
+      chunk_at(q, 40, kK0, 0);
+      chunk_at(q, 80, 1, 1);
+      chunk_at(q, 120, kK0, 0);
+      chunk_at(q, 160, 1, 1);
+      chunk_at(q, 200, kK0, 0);
+      o += 240;
+    }
   }
   // city.c:443-453: rest / 40 whole chunks, then one ending at len when
   // rest % 40 != 0 (rest < 240: at most 6).  Every chunk's load is issued
   // before the first is mixed (one round trip instead of up to six).
   {
+    const u32 o = (u32)(blocks * 240);
+    const u64 rest = len - blocks * 240;
     const u32 nt = (u32)(rest / 40) + (rest % 40 ? 1u : 0u);
     Words<10> tw[6];
 #pragma unroll
@@ -629,8 +728,12 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
       if ((u32)k < nt) tw[k] = s.template span<40>((u32)k < rest / 40 ? o + 40u * k : (u32)len - 40u);
 #pragma unroll
     for (int k = 0; k < 6; ++k)
-      if ((u32)k < nt) chunk(tw[k].w64(0), tw[k].w64(8), tw[k].w64(16), tw[k].w64(24), tw[k].w64(32), kK0, 0);
+      if ((u32)k < nt)
+        st.chunk(tw[k].w64(0), tw[k].w64(8), tw[k].w64(16), tw[k].w64(24), tw[k].w64(32), kK0, 0, T);
   }
+  // city.c:454-472
+  u64 a = st.a, b = st.b, c = st.c, d = st.d, e = st.e, f = st.f, g = st.g, h = st.h, i = st.i, j = st.j,
+      t = st.t;
   j += i << 32;
   a = mix16(a, j);
   h += g << 32;

@@ -132,11 +132,34 @@ typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 // slower: every 16-B piece refetched its line -- and CityHash128's 16-B
 // shifted loop on line spans -- 5 % slower; both removed in r03.)
 constexpr int kLongLines = 5;
+// NT = kLongStream (r04): as kLongLines for CityHash64 and CityHash128, and
+// CityHashCrc256Long's block loop as a stream of whole 128-B lines
+// (city_core.h crc256_stream_blocks) instead of 256-B line spans.
+constexpr int kLongStream = 6;
 template <bool A16 = false, int NT = 0>
 struct GlobalReaderT {
   static constexpr bool kLines = NT == kLongLines;
-  static constexpr bool kPairs = NT == kLongLines;
+  static constexpr bool kPairs = NT == kLongLines || NT == kLongStream;
+  static constexpr bool kStream = A16 && NT == kLongStream;
   const uint8_t *p;
+  // N bytes at o (16-B aligned key and offset), only the 16-B pieces that
+  // start below lim (the rest zero): a key's last partial line without a
+  // read past round16(len), which the 16-B aligned row stride still covers
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> line_lim(u32 o, u32 lim) const {
+    static_assert(N % 16 == 0, "whole 16-B pieces");
+    gu32x4 *q = reinterpret_cast<gu32x4 *>(reinterpret_cast<uintptr_t>(p + o));
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 16; ++j) {
+      const u32x4 v = o + 16 * j < lim ? q[j] : u32x4{0, 0, 0, 0};
+      w.d[4 * j + 0] = v.x;
+      w.d[4 * j + 1] = v.y;
+      w.d[4 * j + 2] = v.z;
+      w.d[4 * j + 3] = v.w;
+    }
+    return w;
+  }
   template <int N>
   __device__ __forceinline__ Words<N / 4> span(u32 o) const {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p + o);

@@ -211,6 +211,17 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
     // window): per-lane global reads, the 6-bit tables in LDS, 8 WG/CU
     // (VGPR-bound to 3 waves per SIMD)
     const unsigned g = grid_for(blocks, 8, dev);
+#ifdef PDHT_HIP_TUNING
+    if (al16 && stride % 16 == 0 && (tuning_variant() == 190 || tuning_variant() == 191)) {
+      // CityHashCrc256Long's block loop as a 128-B line stream (kLongStream)
+      const int pc = tuning_variant() == 190 ? 8 : 4;
+      g_kernel = pc == 8 ? "k_global<fixed,a16,stream>@8" : "k_global<fixed,a16,stream>@4";
+      k_global<false, Algo, SinkNt, true, kLongStream><<<grid_for(blocks, pc, dev), kBlock, 0, st>>>(
+          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+#endif
     if (al16 && stride % 16 == 0) {
       g_kernel = "k_global<fixed,a16,lines>@8";
       k_global<false, Algo, SinkNt, true, kLongLines><<<g, kBlock, 0, st>>>(k, nullptr, 0, stride, keylen, n,

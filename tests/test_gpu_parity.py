@@ -144,6 +144,28 @@ def test_crc128_long_keys_6bit_tables(dev, oracle, L):
     assert (got == oracle.city128_fixed(k, crc=True)).all()
 
 
+@pytest.mark.tuning
+@pytest.mark.parametrize("variant", [190, 191])
+@pytest.mark.parametrize("L", [901, 960, 1000, 1024, 1100, 1919, 1920, 2200, 4096])
+def test_crc128_long_keys_line_stream(dev, oracle, L, variant):
+    """Tuning variants 190/191: CityHashCrc256Long's block loop as a stream of
+    128-B lines.  Rows padded to a 16-B stride (the 16-B aligned path), the
+    last key at the very end of its allocation; seeded variant too."""
+    rng = np.random.default_rng(L + variant)
+    n, S = 3001, (L + 15) // 16 * 16
+    rows = rng.integers(0, 256, (n, S), dtype=np.uint8)
+    k = np.ascontiguousarray(rows[:, :L])
+    kd = to_dev(rows, dev)[:, :L]
+    with P.tuning(variant):
+        got = u64(P.citycrc128_batch(kd))
+        kern = P.last_kernel()
+        s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
+        gs = u64(P.citycrc128_seed_batch(kd[:200], (s0, s1))).reshape(-1, 2)
+    assert kern.startswith("k_global<fixed,a16,stream>")
+    assert (got == oracle.city128_fixed(k, crc=True)).all()
+    assert [tuple(int(x) for x in g) for g in gs] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:200]]
+
+
 @pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 256, 300, 384, 400, 1200])
 def test_seeded_batches(dev, oracle, L):
     rng = np.random.default_rng(77 + L)
