@@ -832,6 +832,8 @@ __device__ __forceinline__ void digit_starts(const RunTab<false> &run, u32 ND, u
 // (1024 keys over 32 digits: 32-key runs), and small sub-tiles keep LDS and
 // VGPRs per workgroup low, so that several workgroups per CU overlap one
 // another's load / rank / store phases.
+// r02-r03 shape of both passes (4 waves x 8 keys per lane, 4 WG/CU); since r04
+// pass 1 runs 8 x 8 @ 2 and 16-B keys' pass 2 too (launch_two_pass_sel).
 constexpr int kTpW = 4, kTpKPL = 8, kTpPerCu = 4;
 template <int W, int KPL>
 constexpr size_t pass1_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 2 + 1); }

@@ -132,28 +132,32 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
 
 
 
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false>
+// Pass 1 and pass 2 each take a shape: W waves x KPL keys per lane per
+// sub-tile, PER_CU workgroups per CU (pass 1: W1, KPL1, PER_CU1).
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false,
+          int W1 = W, int KPL1 = KPL, int PER_CU1 = PER_CU>
 static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
                            u32 *tickets) {
   static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
-  constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;  // waves per SIMD
-  const size_t b1 = pass1_lds_bytes<W, KPL>(), b2 = pass2_lds_bytes<W, KPL>();
-  auto f1 = &k_bucket_pass1<L, W, KPL, WPE, DBG, DYN>;
+  constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;      // waves per SIMD, pass 2
+  constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;  // pass 1
+  const size_t b1 = pass1_lds_bytes<W1, KPL1>(), b2 = pass2_lds_bytes<W, KPL>();
+  auto f1 = &k_bucket_pass1<L, W1, KPL1, WPE1, DBG, DYN>;
   auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, DYN>;
-  auto f1s = &k_bucket_pass1<L, W, KPL, WPE, DBG, false>;
+  auto f1s = &k_bucket_pass1<L, W1, KPL1, WPE1, DBG, false>;
   auto f2s = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, false>;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1s), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2s), b2)) return rc;
   const u64 cus = (u64)std::max(1, g_dev[dev].cus);
-  unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU);
+  unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU1);
   if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
   // (tickets need a grid that is a multiple of 8; small grids: static order)
   if (DYN && g1 % 8 == 0)
-    f1<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp, tickets);
+    f1<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp, tickets);
   else
-    f1s<<<g1, W * 64, b1, st>>>(a.k, a.n, a.rk, tp, nullptr);
+    f1s<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp, nullptr);
   unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
   if (g2 >= 8) g2 &= ~7u;
   if (DYN && g2 % 8 == 0)
@@ -167,9 +171,35 @@ static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &ou
 template <int L, class Out>
 static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
                                u32 *tickets) {
-  // (r02 A/B of sub-tile shapes, 8 x 4 / 4 x 16 / 4 x 4 keys and 2-6 WG/CU,
-  // and of per-XCD tile tickets: the product shape was best or equal)
-  return launch_two_pass<L, Out>(a, tp, out, st, dev, tickets);
+  // Shapes (waves x keys per lane per sub-tile @ workgroups per CU).  r02's
+  // A/B (8 x 4 / 4 x 16 / 4 x 4 keys, 2-6 WG/CU, per-XCD tile tickets) kept
+  // 4 x 8 @ 4 for both passes.  r04, interleaved, after the fine-plus digit
+  // split had moved work into pass 1 (profiles/r04/ab/bucket_*_tp_shapes*.log):
+  // pass 1 in 8 x 8 @ 2 (4096-key sub-tiles = one counting tile, runs twice as
+  // long, half the barriers per key): 8-B keys at 8192 / 2048 ranks -11 /
+  // -10.5 %, 32-B at 4096 -4 %; 16-B keys gain most with pass 2 in 8 x 8 @ 2
+  // as well (-9 % at 4096 ranks; 8-B keys +4 % with it).  Pass 2 in 8 x 8 @ 3
+  // or 16 x 4 @ 2, pass 1 in 4 x 16 / 16 x 4 / 8 x 4: slower.
+#ifdef PDHT_HIP_TUNING
+  switch (tuning_variant()) {  // r04: the shapes again, per pass, on the fine-plus digit split
+    case 192: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 4, 16, 3>(a, tp, out, st, dev, tickets);
+    case 193: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    case 194: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 3>(a, tp, out, st, dev, tickets);
+    case 195: return launch_two_pass<L, Out, 4, 16, 3>(a, tp, out, st, dev, tickets);
+    case 196: return launch_two_pass<L, Out, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    case 197: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 16, 4, 2>(a, tp, out, st, dev, tickets);
+    case 198: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 4, 4>(a, tp, out, st, dev, tickets);
+    case 199: return launch_two_pass<L, Out, 8, 4, 4, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    case 200: return launch_two_pass<L, Out, 8, 8, 3, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    case 201: return launch_two_pass<L, Out, 16, 4, 2, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    case 202: return launch_two_pass<L, Out>(a, tp, out, st, dev, tickets);  // r02-r03: 4 x 8 @ 4 both
+    default: break;
+  }
+#endif
+  if constexpr (L == 16)
+    return launch_two_pass<L, Out, 8, 8, 2, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+  else
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
 }
 
 enum class BucketKernel { kStaged, kGeneric, kTwoPass };

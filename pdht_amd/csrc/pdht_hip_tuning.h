@@ -55,6 +55,12 @@ extern "C" {
  *                 71  two passes from 2 ranks up
  *              83/87  owner-table ranking on 8 x 16 / 4 x 16 tiles, any nranks
  *              85/89  ballot ranking, any nranks (85: static tile order)
+ *            192-196  two-pass sub-tile shapes (waves x keys per lane @ WG/CU): pass 1
+ *                     4x16@3 / 8x8@2 / 8x8@3 (pass 2 as shipped); both passes
+ *                     4x16@3 / 8x8@2 (product: 4x8@4 for both); 197/198 pass 1
+ *                     16x4@2 / 8x4@4; 199-201 pass 1 8x8@2 with pass 2 8x4@4 /
+ *                     8x8@3 / 16x4@2; 202 the r02-r03 shape (4x8@4 both passes;
+ *                     product since r04: pass 1 8x8@2, pass 2 4x8@4 (16-B keys 8x8@2))
  *                164  two-pass arrays of 8/16-B keys on the balanced digit split
  *                     F = 2^ceil(nbits/2) (product: one fine bit more)
  *   records      112  r02 store order (header halves a staging round early)

@@ -524,6 +524,9 @@ BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535
 BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
                  for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
+# 192-196: two-pass sub-tile shapes per pass (r04)
+BUCKET_CASES += [(L, nr, n, v) for v in range(192, 203) for L in (8, 16, 32) for nr in (2049, 8192)
+                 for n in (4095, 300007, (1 << 20) + 5)]
 # 164: two-pass arrays on the balanced digit split (the product takes one fine bit more)
 BUCKET_CASES += [(L, nr, n, 164) for L in (8, 16, 32) for nr in (1025, 2049, 4097, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
