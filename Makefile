@@ -33,7 +33,14 @@ OBJ     := $(OBJ_ENG) $(LIBDIR)/pdht_hash.o
 OBJ_MPI := $(OBJ_ENG) $(LIBDIR)/pdht_hash_mpi.o
 OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
 
-.PHONY: all product oracle clean asm
+# Compile-time experiments for tools/abbench.py (`--variants x0` = variant 0
+# of this build): the tuning build plus EXP flags, e.g.
+#   make exp EXP=-DPDHT_MUL_MAD
+LIB_EXP := $(LIBDIR)/libpdht_hip_exp.so
+EXP ?=
+OBJ_EXP := $(HIP_UNITS:%=$(LIBDIR)/%.exp.o) $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash.o
+
+.PHONY: all product oracle clean asm exp
 all: product oracle
 
 product: $(LIB) $(LIB_MPI) $(LIB_TUN)
@@ -49,6 +56,15 @@ $(LIBDIR)/%.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 $(LIBDIR)/%.tun.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DPDHT_HIP_TUNING -c -o $@ $<
+
+$(LIBDIR)/%.exp.o: pdht_amd/csrc/%.hip $(HIP_HDR) FORCE
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DPDHT_HIP_TUNING $(EXP) -c -o $@ $<
+
+exp: $(OBJ_EXP)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIB_EXP) $(OBJ_EXP)
+
+FORCE:
 
 $(LIBDIR)/pdht_hash.o: pdht_amd/host/pdht_hash.c $(SHIM_HDR)
 	@mkdir -p $(LIBDIR)
@@ -76,5 +92,5 @@ asm:
 	for u in $(HIP_UNITS); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/$$u.s pdht_amd/csrc/$$u.hip || exit 1; done
 
 clean:
-	rm -f $(LIBDIR)/*.o $(LIB) $(LIB_MPI) $(LIB_TUN)
+	rm -f $(LIBDIR)/*.o $(LIB) $(LIB_MPI) $(LIB_TUN) $(LIB_EXP)
 	$(MAKE) -s -C oracle clean

@@ -73,11 +73,15 @@ class _PdhtT(C.Structure):
 _lib = None        # the library the wrappers call (product, or tuning inside tuning())
 _product = None
 _tuning = None
+_exp = None  # libpdht_hip_exp.so (tools/ only)
 _V = C.c_void_p
 _S = C.c_size_t
 _U64 = C.c_uint64
 _U32 = C.c_uint32
 TUNING_LIB_PATH = os.path.join(HERE, "lib", "libpdht_hip_tuning.so")
+# tools/ only: the tuning build with a compile-time experiment switched on
+# (`make exp EXP=-DPDHT_...`), for A/B of changes a run-time variant cannot select
+EXP_LIB_PATH = os.path.join(HERE, "lib", "libpdht_hip_exp.so")
 MPI_LIB_PATH = os.path.join(HERE, "lib", "libpdht_hip_mpi.so")
 
 
@@ -177,24 +181,30 @@ class tuning:
     kernel variant `variant` and, optionally, `per_cu` workgroups per CU.
     The product library has no variants and no tuning entry points."""
 
-    def __init__(self, variant: int = 0, per_cu: int = 0):
-        self.variant, self.per_cu = variant, per_cu
+    def __init__(self, variant: int = 0, per_cu: int = 0, exp: bool = False):
+        self.variant, self.per_cu, self.exp = variant, per_cu, exp
 
     def __enter__(self):
-        global _lib, _tuning
+        global _lib, _tuning, _exp
         lib()
-        if _tuning is None:
-            _tuning = _load(TUNING_LIB_PATH, tuning=True)
+        if self.exp:
+            if _exp is None:
+                _exp = _load(EXP_LIB_PATH, tuning=True)
+            self._t = _exp
+        else:
+            if _tuning is None:
+                _tuning = _load(TUNING_LIB_PATH, tuning=True)
+            self._t = _tuning
         self._prev = _lib
-        self._old = (_tuning.pdht_hip_set_variant(self.variant),
-                     _tuning.pdht_hip_set_blocks_per_cu(self.per_cu))
-        _lib = _tuning
+        self._old = (self._t.pdht_hip_set_variant(self.variant),
+                     self._t.pdht_hip_set_blocks_per_cu(self.per_cu))
+        _lib = self._t
         return self
 
     def __exit__(self, *exc):
         global _lib
-        _tuning.pdht_hip_set_variant(self._old[0])
-        _tuning.pdht_hip_set_blocks_per_cu(self._old[1])
+        self._t.pdht_hip_set_variant(self._old[0])
+        self._t.pdht_hip_set_blocks_per_cu(self._old[1])
         _lib = self._prev
         return False
 

@@ -50,11 +50,19 @@ PDHT_HD u64 rotr_nz(u64 v, u32 s) { return (v >> s) | (v << (64 - s)); }
 PDHT_HD u64 rotr(u64 v, u32 s) { return s == 0 ? v : rotr_nz(v, s); }
 PDHT_HD u64 smix(u64 v) { return v ^ (v >> 47); }  // city.c:127-129
 
+// u64 x u64, low 64 bits (every CityHash multiply goes through here).  The
+// compiler emits v_mad_u64_u32 (lo x lo) + 2 v_mul_lo_u32 + v_add3_u32; r04
+// tried three v_mad_u64_u32 instead (each cross term folded into the high
+// half): 81 -> 85 mul VALU on the 64-B Crc128 hash but +49 v_mov_b32 to
+// zero-extend the addends, so more cycles (the `make exp` A/B build keeps the
+// switch point).
+PDHT_HD u64 mul64(u64 a, u64 b) { return a * b; }
+
 // city.c:101-110 Hash128to64 == city.c:131-136 HashLen16(u, v)
 PDHT_HD u64 mix16(u64 u, u64 v) {
-  u64 a = smix((u ^ v) * kMul);
-  u64 b = smix((v ^ a) * kMul);
-  return b * kMul;
+  u64 a = smix(mul64((u ^ v), kMul));
+  u64 b = smix(mul64((v ^ a), kMul));
+  return mul64(b, kMul);
 }
 
 // ------------------------------------------------------------ key windows ---
@@ -167,7 +175,7 @@ PDHT_HD u64 len0to16(const R &s, u64 len) {
     const u32 a = s.b8(0), b = s.b8(n >> 1), c = s.b8(n - 1);
     const u32 y = a + (b << 8);
     const u32 z = n + (c << 2);
-    return smix((u64)y * kK2 ^ (u64)z * kK3) * kK2;
+    return mul64(smix((u64)mul64(y, kK2) ^ (u64)mul64(z, kK3)), kK2);
   }
   return kK2;
 }
@@ -177,10 +185,10 @@ template <class R>
 PDHT_HD u64 len17to32(const R &s, u64 len) {
   const Words<4> h = s.template span<16>(0);
   const Words<4> t = s.template span<16>((u32)len - 16);
-  const u64 a = h.w64(0) * kK1;
+  const u64 a = mul64(h.w64(0), kK1);
   const u64 b = h.w64(8);
-  const u64 c = t.w64(8) * kK2;
-  const u64 d = t.w64(0) * kK0;
+  const u64 c = mul64(t.w64(8), kK2);
+  const u64 d = mul64(t.w64(0), kK0);
   return mix16(rotr_nz(a - b, 43) + rotr_nz(c, 30) + d,
                a + rotr_nz(b ^ kK3, 20) - c + len);
 }
@@ -206,7 +214,7 @@ PDHT_HD u64 len33to64(const R &s, u64 len) {
   const Words<8> h = s.template span<32>(0);
   const Words<8> t = s.template span<32>((u32)len - 32);
   u64 z = h.w64(24);
-  u64 a = h.w64(0) + (len + t.w64(16)) * kK0;
+  u64 a = h.w64(0) + mul64((len + t.w64(16)), kK0);
   u64 b = rotr_nz(a + z, 52);
   u64 c = rotr_nz(a, 37);
   a += h.w64(8);
@@ -223,8 +231,8 @@ PDHT_HD u64 len33to64(const R &s, u64 len) {
   a += t.w64(16);
   const u64 wf = a + z;
   const u64 ws = b + rotr_nz(a, 31) + c;
-  const u64 r = smix((vf + ws) * kK2 + (wf + vs) * kK0);
-  return smix(r * kK0 + vs) * kK2;
+  const u64 r = smix(mul64((vf + ws), kK2) + mul64((wf + vs), kK0));
+  return mul64(smix(mul64(r, kK0) + vs), kK2);
 }
 
 // 56 bytes of running state of the >64-byte loops (city.c:236-260, :315-350)
@@ -236,12 +244,12 @@ struct LongState {
 // One 64-byte round over chunk c, including the z<->x exchange
 // (city.c:248-257 == :329-338 == :340-349).
 PDHT_HD void round64(LongState &st, const Words<16> &c) {
-  u64 x = rotr_nz(st.x + st.y + st.v.lo + c.w64(8), 37) * kK1;
-  u64 y = rotr_nz(st.y + st.v.hi + c.w64(48), 42) * kK1;
+  u64 x = mul64(rotr_nz(st.x + st.y + st.v.lo + c.w64(8), 37), kK1);
+  u64 y = mul64(rotr_nz(st.y + st.v.hi + c.w64(48), 42), kK1);
   x ^= st.w.hi;
   y += st.v.lo + c.w64(40);
-  const u64 z = rotr_nz(st.z + st.w.lo, 33) * kK1;
-  const u128 v = weak32_at(c, 0, st.v.hi * kK1, x + st.w.lo);
+  const u64 z = mul64(rotr_nz(st.z + st.w.lo, 33), kK1);
+  const u128 v = weak32_at(c, 0, mul64(st.v.hi, kK1), x + st.w.lo);
   const u128 w = weak32_at(c, 32, z + st.w.hi, y + c.w64(16));
   st.v = v;
   st.w = w;
@@ -259,12 +267,12 @@ PDHT_HD void city64_long_init(const Words<16> &t, u64 len, LongState &st) {
   st.z = mix16(t.w64(16) + len, t.w64(40));
   st.v = weak32_at(t, 0, len, st.z);
   st.w = weak32_at(t, 32, st.y + kK1, x);
-  st.x = x * kK1;
+  st.x = mul64(x, kK1);
 }
 
 // city.c:261-262
 PDHT_HD u64 city64_long_final(const LongState &st) {
-  return mix16(mix16(st.v.lo, st.w.lo) + smix(st.y) * kK1 + st.z, mix16(st.v.hi, st.w.hi) + st.x);
+  return mix16(mix16(st.v.lo, st.w.lo) + mul64(smix(st.y), kK1) + st.z, mix16(st.v.hi, st.w.hi) + st.x);
 }
 
 // Readers that set kPairs read the >64-byte loop two rounds (128 B, a whole
@@ -319,8 +327,8 @@ template <class R>
 PDHT_HD u128 murmur128(const R &s, u64 len, u128 seed) {
   u64 a = seed.lo, b = seed.hi, c, d;
   if (len <= 16) {
-    a = smix(a * kK1) * kK1;
-    c = b * kK1 + len0to16(s, len);
+    a = mul64(smix(mul64(a, kK1)), kK1);
+    c = mul64(b, kK1) + len0to16(s, len);
     d = smix(a + (len >= 8 ? fetch64(s, 0) : c));
   } else {
     const u32 n = (u32)len;
@@ -331,10 +339,10 @@ PDHT_HD u128 murmur128(const R &s, u64 len, u128 seed) {
     const u32 steps = (n - 1) >> 4;  // signed l = len-16; do..while (l > 0)
     for (u32 k = 0; k < steps; ++k) {
       const Words<4> q = s.template span<16>(16 * k);
-      a ^= smix(q.w64(0) * kK1) * kK1;
+      a ^= mul64(smix(mul64(q.w64(0), kK1)), kK1);
       a *= kK1;
       b ^= a;
-      c ^= smix(q.w64(8) * kK1) * kK1;
+      c ^= mul64(smix(mul64(q.w64(8), kK1)), kK1);
       c *= kK1;
       d ^= c;
     }
@@ -356,8 +364,8 @@ template <class R>
 PDHT_HD u128 city128_finish(const R &s, u32 o, u64 rem, const LongState &st) {
   u64 x = st.x, y = st.y, z = st.z;
   u128 v = st.v, w = st.w;
-  x += rotr_nz(v.lo + z, 49) * kK0;
-  z += rotr_nz(w.lo, 37) * kK0;
+  x += mul64(rotr_nz(v.lo + z, 49), kK0);
+  z += mul64(rotr_nz(w.lo, 37), kK0);
   // city.c:357-365: up to 4 chunks of 32 B from the end.  All four are
   // loaded before the first is used (one memory round trip, not four); the
   // unused ones stay inside the key, since o >= 128 when rem > 0.
@@ -369,9 +377,9 @@ PDHT_HD u128 city128_finish(const R &s, u32 o, u64 rem, const LongState &st) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (32u * k >= (u32)rem) break;
-    y = rotr_nz(x + y, 42) * kK0 + v.hi;
+    y = mul64(rotr_nz(x + y, 42), kK0) + v.hi;
     w.lo += p[k].w64(16);
-    x = x * kK0 + w.lo;
+    x = mul64(x, kK0) + w.lo;
     z += w.hi + p[k].w64(0);
     w.hi += v.lo;
     v = weak32_at(p[k], 0, v.lo + z, v.hi);
@@ -389,12 +397,12 @@ PDHT_HD u128 city128_seed_lines(const R &b, u64 len, u128 seed) {
   LongState st;
   st.x = seed.lo;
   st.y = seed.hi;
-  st.z = len * kK1;
+  st.z = mul64(len, kK1);
   Words<32> l0 = b.template span<128>(0);  // len >= 128
-  st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + l0.w64(0);
-  st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + l0.w64(8);
-  st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
-  st.w.hi = rotr_nz(st.x + l0.w64(88), 53) * kK1;
+  st.v.lo = mul64(rotr_nz(st.y ^ kK1, 49), kK1) + l0.w64(0);
+  st.v.hi = mul64(rotr_nz(st.v.lo, 42), kK1) + l0.w64(8);
+  st.w.lo = mul64(rotr_nz(st.y + st.z, 35), kK1) + st.x;
+  st.w.hi = mul64(rotr_nz(st.x + l0.w64(88), 53), kK1);
   u32 o = 0;
   u64 rem = len;
   do {
@@ -415,14 +423,14 @@ PDHT_HD u128 city128_seed(const R &s, u64 len, u128 seed) {
   LongState st;
   st.x = seed.lo;
   st.y = seed.hi;
-  st.z = len * kK1;
+  st.z = mul64(len, kK1);
   {
     const Words<4> h = s.template span<16>(0);
-    st.v.lo = rotr_nz(st.y ^ kK1, 49) * kK1 + h.w64(0);
-    st.v.hi = rotr_nz(st.v.lo, 42) * kK1 + h.w64(8);
+    st.v.lo = mul64(rotr_nz(st.y ^ kK1, 49), kK1) + h.w64(0);
+    st.v.hi = mul64(rotr_nz(st.v.lo, 42), kK1) + h.w64(8);
   }
-  st.w.lo = rotr_nz(st.y + st.z, 35) * kK1 + st.x;
-  st.w.hi = rotr_nz(st.x + fetch64(s, 88), 53) * kK1;
+  st.w.lo = mul64(rotr_nz(st.y + st.z, 35), kK1) + st.x;
+  st.w.hi = mul64(rotr_nz(st.x + fetch64(s, 88), 53), kK1);
   u32 o = 0;
   u64 rem = len;
   do {
@@ -443,7 +451,7 @@ PDHT_HD u128 city128(const R &s, u64 len) {
   }
   if (len >= 8) {
     // WithSeed(NULL, 0, seed): no key byte is read after the seed is formed
-    const u128 seed{fetch64(s, 0) ^ (len * kK0), fetch64(s, (u32)len - 8) ^ kK1};
+    const u128 seed{fetch64(s, 0) ^ (mul64(len, kK0)), fetch64(s, (u32)len - 8) ^ kK1};
     return murmur128(s, 0, seed);
   }
   return murmur128(s, len, u128{kK0, kK1});
@@ -581,11 +589,11 @@ struct Crc256State {
   u64 a, b, c, d, e, f, g, h, i, j, t;
   PDHT_HD void chunk(u64 w0, u64 w1, u64 w2, u64 w3, u64 w4, u64 mult, u32 flip, const Tab &T) {
     const u64 a0 = a;
-    a = rotr(b, 41u ^ flip) * mult + w0;
-    b = rotr(c, 27u ^ flip) * mult + w1;
-    c = rotr(d, 41u ^ flip) * mult + w2;
-    d = rotr(e, 33u ^ flip) * mult + w3;
-    e = rotr(t, 25u ^ flip) * mult + w4;
+    a = mul64(rotr(b, 41u ^ flip), mult) + w0;
+    b = mul64(rotr(c, 27u ^ flip), mult) + w1;
+    c = mul64(rotr(d, 41u ^ flip), mult) + w2;
+    d = mul64(rotr(e, 33u ^ flip), mult) + w3;
+    e = mul64(rotr(t, 25u ^ flip), mult) + w4;
     t = a0;
     f = crc32c_u64(f, a, T);
     g = crc32c_u64(g, b, T);
@@ -658,7 +666,7 @@ PDHT_HD void crc256_stream_blocks(const R &s, u64 len, u32 seed, u64 out[4], Crc
   st.a = S.A.w64(56) + kK0;
   st.b = S.A.w64(96) + kK0;
   st.c = out[0] = mix16(st.b, len);
-  st.d = out[1] = S.A.w64(120) * kK0 + len;
+  st.d = out[1] = mul64(S.A.w64(120), kK0) + len;
   st.e = S.B.w64(56) + seed;
   st.f = seed;
   st.g = st.h = st.i = st.j = 0;
@@ -688,7 +696,7 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
     st.a = q.w64(56) + kK0;
     st.b = q.w64(96) + kK0;
     st.c = out[0] = mix16(st.b, len);
-    st.d = out[1] = q.w64(120) * kK0 + len;
+    st.d = out[1] = mul64(q.w64(120), kK0) + len;
     st.e = q.w64(184) + seed;
     st.f = seed;
     st.g = st.h = st.i = st.j = 0;
@@ -746,11 +754,11 @@ PDHT_HD void crc256_long(const R &s, u64 len, u32 seed, u64 out[4], const Tab &T
   f = mix16(b, c) + a;
   g = mix16(j, i) + c;
   out[0] = e + f + g + h;
-  a = smix((a + g) * kK0) * kK0 + b;
+  a = mul64(smix(mul64((a + g), kK0)), kK0) + b;
   out[1] += a + out[0];
-  a = smix(a * kK0) * kK0 + c;
+  a = mul64(smix(mul64(a, kK0)), kK0) + c;
   out[2] = a + out[1];
-  a = smix((a + e) * kK0) * kK0;
+  a = mul64(smix(mul64((a + e), kK0)), kK0);
   out[3] = a + out[2];
 }
 
@@ -772,7 +780,7 @@ PDHT_HD u128 crc128_seed(const R &s, u64 len, u128 seed, const Tab &T = Tab{}) {
   crc256(s, len, r, T);
   const u64 u = seed.hi + r[0];
   const u64 v = seed.lo + r[1];
-  return u128{mix16(u, v + r[2]), mix16(rotr_nz(v, 32), u * kK0 + r[3])};
+  return u128{mix16(u, v + r[2]), mix16(rotr_nz(v, 32), mul64(u, kK0) + r[3])};
 }
 
 // city.c:506-517

@@ -147,11 +147,14 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     step, result, nbytes = workload(a.work, dev)
-    combos = [(int(v), int(pc)) for v in a.variants.split(",") for pc in a.per_cu.split(",")]
+    # "x<N>" = variant N of the compile-time experiment build (make exp EXP=...)
+    combos = [(v, int(pc)) for v in a.variants.split(",") for pc in a.per_cu.split(",")]
 
     class Ctx:
         def __init__(self, v, pc):
-            self.c = P.tuning(v, pc) if (v or pc) else None
+            x = str(v).startswith("x")
+            n = int(str(v)[1:] if x else v)
+            self.c = P.tuning(n, pc, exp=True) if x else P.tuning(n, pc) if (n or pc) else None
 
         def __enter__(self):
             if self.c:
