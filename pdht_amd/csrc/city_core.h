@@ -53,7 +53,7 @@ PDHT_HD u64 smix(u64 v) { return v ^ (v >> 47); }  // city.c:127-129
 // u64 x u64, low 64 bits (every CityHash multiply goes through here).  The
 // compiler emits v_mad_u64_u32 (lo x lo) + 2 v_mul_lo_u32 + v_add3_u32; r04
 // tried three v_mad_u64_u32 instead (each cross term folded into the high
-// half): 81 -> 85 mul VALU on the 64-B Crc128 hash but +49 v_mov_b32 to
+// half): 112 -> 85 multiply VALU on the 64-B Crc128 hash but +49 v_mov_b32 to
 // zero-extend the addends, so more cycles (the `make exp` A/B build keeps the
 // switch point).
 PDHT_HD u64 mul64(u64 a, u64 b) { return a * b; }
