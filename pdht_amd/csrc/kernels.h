@@ -686,7 +686,7 @@ __device__ __forceinline__ u32 xpose_slot(u32 k, u32 c) { return 4 * k + (c ^ ((
 // 4 contiguous 16-B pieces of the NEXT tile (global_load_dwordx4, 1 KiB per
 // wave-instruction) while the current tile hashes, then writes them into the
 // image with ds_write_b128.
-template <class Algo, class Sink, bool LNT = false, int DEPTH = 1, int BLOCK = kBlock>
+template <class Algo, class Sink, bool LNT = false, int DEPTH = 1, int BLOCK = kBlock, int PRIO = 0>
 __global__ __launch_bounds__(BLOCK) void k_fixed_xpose64(const uint8_t *__restrict__ keys, u64 n,
                                                          Algo algo, Sink sink) {
   constexpr int kWavesPerBlock = BLOCK / 64;
@@ -727,7 +727,9 @@ __global__ __launch_bounds__(BLOCK) void k_fixed_xpose64(const uint8_t *__restri
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const u64 tn = tt + DEPTH * nwaves;
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
         if (tn < full) fetch(d, tn);  // refill this register set while hashing
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         const u32 sw = (lane >> 2) & 3;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -752,7 +754,10 @@ __global__ __launch_bounds__(BLOCK) void k_fixed_xpose64(const uint8_t *__restri
 // Any key length.  VAR: key i = bytes[offsets[i]-obase, offsets[i+1]-obase);
 // otherwise key i = bytes[i*stride, i*stride+keylen).  WIN = LDS bytes per
 // wave.  AUX = cache-policy bits of the LDS-DMA (2 = non-temporal).
-template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0, int ALIGN = 16, class LR = LdsReader>
+// PRIO (tuning): the wave raises its issue priority while it fetches the
+// next tile's offsets and issues the window DMA, and drops it to hash.
+template <int WIN, bool VAR, class Algo, class Sink, int AUX = 0, int ALIGN = 16, class LR = LdsReader,
+          int PRIO = 0>
 __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ bytes,
                                                    const u64 *__restrict__ offsets, u64 obase,
                                                    u64 stride, u64 keylen, u64 n, Algo algo,
@@ -773,6 +778,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
   const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
   u32 *lds = win_all + wave * (WIN / 4);
   for (u64 t = (u64)blockIdx.x * kWavesPerBlock + wave; t < ntiles; t += nwaves) {
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
     const u64 k0 = t << 6;
     const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;  // one past the tile's last key
     const u64 i = k0 + lane;
@@ -817,6 +823,7 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
               (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, AUX);
       }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     if (valid) {

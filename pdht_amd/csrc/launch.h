@@ -165,6 +165,13 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
         HIP_TRY(hipGetLastError());
         return 0;
       }
+      if (tuning_variant() == 206) {  // s_setprio 1 around each wave's prefetch issue
+        g_kernel = "k_fixed_xpose64<nt,d2,prio1>@3";
+        k_fixed_xpose64<Algo, SinkNt, true, 2, kBlock, 1><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
+            k, n, algo, sink_nt);
+        HIP_TRY(hipGetLastError());
+        return 0;
+      }
       if constexpr (std::is_same<Sink, Sink64>::value) {
         if (tuning_variant() == 188) {  // digests stored 16 B per lane (even lanes, DPP pairs)
           g_kernel = "k_fixed_xpose64<nt,d2,st16>@3";
@@ -342,6 +349,17 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
       HIP_TRY(hipGetLastError());
       return 0;
     }
+    if (v == 203 || v == 204) {  // the product window kernel, s_setprio around the fetch phase
+      g_kernel = v == 203 ? "k_window<var,nt,10224,prio3>@4" : "k_window<var,nt,10224,prio1>@4";
+      if (v == 203)
+        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReader, 3><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
+      else
+        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReader, 1><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+            b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
     if (v == 189) {  // the product window kernel, digests stored 16 B per lane
       g_kernel = "k_window<var,nt,10224,st16>@4";
       k_window<10224, true, Algo, Sink64x2T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
@@ -388,9 +406,20 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
     k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,
                                                                                     algo, sink_nt);
   } else {
+    // s_setprio 1 while a wave fetches its next tile's offsets and issues the
+    // window DMA (r04, interleaved: cfg3 +1.8 %, cfg3c +0.8 %; 3 equal to 1;
+    // tuning 205 = without)
     g_kernel = "k_window<var,nt,10224>@4";
-    k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,
-                                                                                    algo, sink_nt);
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 205) {
+      k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0,
+                                                                                      n, algo, sink_nt);
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
+#endif
+    k_window<10224, true, Algo, SinkNt, 2, 16, LdsReader, 1><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
+        b, offsets, obase, 0, 0, n, algo, sink_nt);
   }
   HIP_TRY(hipGetLastError());
   return 0;

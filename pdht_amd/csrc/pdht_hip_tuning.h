@@ -17,6 +17,7 @@ extern "C" {
  *   64-B keys      7  one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
  *                 26  plain instead of non-temporal digest stores (2-6 % slower)
  *                188  digests stored 16 B per lane (even lanes, DPP pairs: Sink64x2T)
+ *                206  s_setprio 1 around each wave's prefetch issue
  *              80/81  1024-thread transpose at 1 / 2 WG/CU (cfg1 shape)
  *                 82  the 256-thread transpose whatever the histogram
  *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
@@ -37,6 +38,8 @@ extern "C" {
  *           110 / 111 (same entry) the window kernel hashing every key twice
  *                     / once: what the arithmetic costs over 40
  *                189  CityHash64 window kernel with 16-B-per-lane digest stores
+ *            203/204  CityHash64 window kernel, s_setprio 3 / 1 while fetching
+ *                205  variable-length window kernel without s_setprio (product: 1)
  *            180-187  k_window_pipe G1 cache policies (DMA / digest stores): nt / plain,
  *                     nt / sc0, nt / sc1, nt / sc1|nt, nt / sc0|sc1|nt, plain / nt,
  *                     sc0|nt / nt, sc1 / nt

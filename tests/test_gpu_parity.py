@@ -190,6 +190,7 @@ def _variants(vs):
 
 
 VARIANT_KERNELS = {0: "k_fixed_xpose64<nt,d2>@3", 7: "k_fixed_xpose64<nt,d1>@4", 188: "k_fixed_xpose64<nt,d2,st16>@3",
+                   206: "k_fixed_xpose64<nt,d2,prio1>@3",
                    26: "k_fixed_xpose64<nt-load,plain-store,d2>@3"}
 
 
@@ -304,7 +305,8 @@ VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,1
                170: "k_window_pipe<var,10224,G1>@4", 171: "k_window_pipe<var,10224,G4>@4",
                172: "k_window_pipe<var,10224,G16>@4", 173: "k_window_pipe<var,10224,G1>@3",
                174: "k_window_pipe<var,10224,G1,funnel>@4", 175: "k_window<var,nt,10224,funnel>@4",
-               189: "k_window<var,nt,10224,st16>@4"}
+               189: "k_window<var,nt,10224,st16>@4", 203: "k_window<var,nt,10224,prio3>@4",
+               204: "k_window<var,nt,10224,prio1>@4", 205: "auto"}  # 205: the product's choice, no s_setprio
 
 
 def auto_var_kernel(total_bytes, n):
@@ -315,9 +317,10 @@ def auto_var_kernel(total_bytes, n):
 @pytest.mark.parametrize("variant", _variants(sorted(VAR_KERNELS)))
 def test_var_edge_cases(dev, oracle, variant):
     with P.tuning(variant) if variant else _nullctx():
-        total, n = _var_edge_cases(dev, oracle, kernel=VAR_KERNELS[variant] if variant >= 170 else None)
-        want = auto_var_kernel(total, n) if variant == 0 else VAR_KERNELS[variant]
-        if variant < 170:  # (170-175: CityHash64 kernels only, checked per call inside)
+        auto = VAR_KERNELS[variant] == "auto"
+        total, n = _var_edge_cases(dev, oracle, kernel=VAR_KERNELS[variant] if variant >= 170 and not auto else None)
+        want = auto_var_kernel(total, n) if auto else VAR_KERNELS[variant]
+        if variant < 170 or auto:  # (170+: CityHash64 kernels only, checked per call inside)
             assert P.last_kernel() == want
 
 
@@ -346,7 +349,7 @@ def test_var_many_tiles_per_wave(dev, oracle, variant):
     with P.tuning(variant) if variant else _nullctx():
         got = u64(P.city64_var_batch(to_dev(data, dev), to_dev(offs.astype(np.int64), dev)))
         kern = P.last_kernel()
-    assert variant == 0 or kern == VAR_KERNELS[variant]
+    assert VAR_KERNELS[variant] == "auto" or kern == VAR_KERNELS[variant]
     assert (got == oracle.city64_var(data, offs)).all()
 
 
