@@ -775,7 +775,8 @@ def check_records(P, torch, D, sh, keys, b, dev, cdev):
     ty, sr, hi, ix32, mb, ko = P.record_fields(rec, keys.shape[1])
     ix = ix32.to(torch.int64) & 0xFFFFFFFF
     msgs, ok, golden = [], True, False
-    g = (golden_folds() or {}).get("bucket_8B_16M", {})
+    folds = golden_folds() or {}
+    g = folds.get("bucket_8B_16M" if nr == 1024 else f"bucket_8B_16M_{nr}", {})
     r = sh.first // (16 * M)
     if nr == g.get("nranks") and n == g.get("n") and sh.first % n == 0 and r < len(g.get("shards", [])):
         gs = g["shards"][r]

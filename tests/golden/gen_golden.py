@@ -19,6 +19,7 @@ the two modulo reductions of hash.c:27 and :29 done in Python.
                                              #   and cfg1 pdht_hash placement folds (added)
   python tests/golden/gen_golden.py --multirank # + per-rank cfg1/cfg3/cfg4 folds of the
                                              #   N > 1 weak-scaling shards (added)
+  python tests/golden/gen_golden.py --bucket-world  # + exchange/xrecords folds (nranks = N)
 """
 from __future__ import annotations
 
@@ -244,6 +245,32 @@ def folds_bucket8k() -> dict:
     return res
 
 
+def folds_bucket_world() -> dict:
+    """exchange / xrecords at N ranks bucket each rank's 16M-key shard by
+    CityHash64 % N (nranks = world size, nptes 3): for N in 1, 2, 4, 8 and
+    every shard r < N, folds of the stably bucketed mbits, of the original
+    indices and of the bucket offsets (the same fields as folds_bucket8k)."""
+    thr = os.cpu_count() or 8
+    worlds = (1, 2, 4, 8)
+    res = {f"bucket_8B_16M_{w}": {"n": 16 * M, "L": 8, "nptes": 3, "nranks": w, "shards": []} for w in worlds}
+    n = 16 * M
+    for r in range(max(worlds)):
+        m = O.apply_ref64(O.fixed_keys(n, 8, first_key=r * n), n, L=8, threads=thr)
+        for w in worlds:
+            if r >= w:
+                continue
+            rk = (m % np.uint64(w)).astype(np.int64)
+            order = np.argsort(rk, kind="stable")
+            offs = np.zeros(w + 1, np.uint64)
+            np.cumsum(np.bincount(rk, minlength=w).astype(np.uint64), out=offs[1:])
+            res[f"bucket_8B_16M_{w}"]["shards"].append({
+                "mbits": f"{O.fold64(m[order], 0):016x}",
+                "index": f"{O.fold64(order.astype(np.uint64), 0):016x}",
+                "offsets": f"{O.fold64(offs, 0):016x}"})
+        print(f"  bucket-by-world shard {r} done", flush=True)
+    return res
+
+
 def r02_vectors(R) -> dict:
     """WeakHashLen32WithSeeds6 / WeakHashLen32WithSeeds (city.c:173-198;
     exported by the reference although city.h does not declare them) on
@@ -334,6 +361,8 @@ def main():
                     help="add the WeakHash vectors (npz) and the cfg1 placement folds (json)")
     ap.add_argument("--bucket8k", action="store_true",
                     help="add the 8192-rank bucketing folds (json)")
+    ap.add_argument("--bucket-world", action="store_true",
+                    help="add the nranks = world-size bucketing folds of exchange/xrecords (json)")
     ap.add_argument("--multirank", action="store_true",
                     help="add per-rank cfg1/cfg3/cfg4 folds of the N > 1 weak-scaling shards (json)")
     a = ap.parse_args()
@@ -352,6 +381,15 @@ def main():
         with open(path, "w") as f:
             json.dump(doc, f, indent=1)
         print("added per-rank cfg1/cfg3/cfg4 folds")
+        return
+    if a.bucket_world:
+        path = os.path.join(HERE, "config_folds.json")
+        with open(path) as f:
+            doc = json.load(f)
+        doc["configs"].update(folds_bucket_world())
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print("added nranks = world bucketing folds")
         return
     if a.bucket8k:
         path = os.path.join(HERE, "config_folds.json")

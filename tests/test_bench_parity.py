@@ -69,6 +69,23 @@ def test_committed_multirank_folds_present():
             assert bench.golden_shard_fold(f, "cfg2", sh)[0] is not None
 
 
+def test_committed_bucket_world_folds():
+    """exchange / xrecords bucket by nranks = world size: a shard for every
+    rank of N = 1, 2, 4, 8.  With one rank the bucketing is the identity:
+    index is 0..n-1, offsets are {0, n}, and mbits fold as the place config's
+    shard 0 (both reference CityHash64 of the same keys at index 0)."""
+    f = bench.golden_folds()
+    n = 16 * bench.M
+    for w in (1, 2, 4, 8):
+        g = f[f"bucket_8B_16M_{w}"]
+        assert g["nranks"] == w and g["n"] == n and len(g["shards"]) == w
+    one = f["bucket_8B_16M_1"]["shards"][0]
+    ident = torch.arange(n, dtype=torch.int64)
+    assert int(one["index"], 16) == D.fold_tensor(ident, 0)
+    assert int(one["offsets"], 16) == D.fold_tensor(torch.tensor([0, n]), 0)
+    assert one["mbits"] == f["place_8B_16M"]["shards"][0]["mbits"]
+
+
 def _parity_worker(rank, world, port, q):
     import os
     import torch.distributed as dist

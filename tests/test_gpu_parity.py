@@ -676,6 +676,29 @@ def test_bucket_records(dev, oracle, L, nranks, n, variant):
     assert (u64(mb) == m2[order]).all() and (ix.cpu().numpy().view(np.uint32) == order).all()
 
 
+@pytest.mark.parametrize("nranks,shard", [(1, 0), (2, 1), (4, 3), (8, 7), (1024, 0), (8192, 5)])
+def test_bucket_shard_golden_folds(dev, folds, nranks, shard):
+    """The bench's bucketing shards at full size (16M x 8-B keys from key
+    shard*16M, nptes 3) against the reference folds: nranks = 1/2/4/8 is what
+    exchange / xrecords bucket at N ranks, 1024 the bucket config, 8192 the
+    two-pass sort.  Arrays and wire records both."""
+    g = folds["bucket_8B_16M" if nranks == 1024 else f"bucket_8B_16M_{nranks}"]
+    assert g["nranks"] == nranks
+    gs = g["shards"][shard]
+    n = g["n"]
+    kd = device_keys(n, 8, first_key=shard * n, dev=dev)
+    ko, mb, pt, ix, offs = P.bucket_batch(kd, 3, nranks)
+    assert f"{gpu_fold(mb):016x}" == gs["mbits"]
+    assert f"{gpu_fold(ix.to(torch.int64) & 0xFFFFFFFF):016x}" == gs["index"]
+    assert f"{gpu_fold(offs):016x}" == gs["offsets"]
+    del ko, pt
+    rec, roffs = P.bucket_records(kd, nranks)
+    _, _, _, rix, rmb, _ = P.record_fields(rec, 8)
+    assert f"{gpu_fold(rmb.contiguous()):016x}" == gs["mbits"]
+    assert f"{gpu_fold(rix.to(torch.int64) & 0xFFFFFFFF):016x}" == gs["index"]
+    assert f"{gpu_fold(roffs):016x}" == gs["offsets"]
+
+
 def test_place_golden_u64_keys(dev, golden):
     keys = np.arange(256, dtype=np.uint64).view(np.uint8).reshape(256, 8)
     kd = to_dev(keys, dev)
