@@ -25,6 +25,8 @@ for step in "$@"; do
              tail -4 gpurun_out/gpu_ttests.log ;;
     ktests)  timeout -k 10 600 $PYT tests -m gpu -k "$K" > gpurun_out/gpu_ktests.log 2>&1; rc=$?
              tail -15 gpurun_out/gpu_ktests.log | cut -c1-300 ;;
+    kttests) timeout -k 10 600 $PYT tests -m gpu -k "$K" --tuning > gpurun_out/gpu_kttests.log 2>&1; rc=$?
+             tail -15 gpurun_out/gpu_kttests.log | cut -c1-300 ;;
     smoke)   timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log; rc=$?
              tail -1 gpurun_out/smoke.log ;;
     bench)   timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
