@@ -35,9 +35,10 @@ OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
 
 # Compile-time experiments for tools/abbench.py (`--variants x0` = variant 0
 # of this build): the tuning build plus EXP flags, e.g.
-#   make exp EXP=-DPDHT_MUL_MAD
-LIB_EXP := $(LIBDIR)/libpdht_hip_exp.so
+#   make exp EXP=-DPDHT_MUL_MAD [EXP_TAG=mad -> libpdht_hip_exp_mad.so, `--variants x0:mad`]
 EXP ?=
+EXP_TAG ?=
+LIB_EXP := $(LIBDIR)/libpdht_hip_exp$(if $(EXP_TAG),_$(EXP_TAG)).so
 OBJ_EXP := $(HIP_UNITS:%=$(LIBDIR)/%.exp.o) $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash.o
 
 .PHONY: all product oracle clean asm exp
@@ -92,5 +93,5 @@ asm:
 	for u in $(HIP_UNITS); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/$$u.s pdht_amd/csrc/$$u.hip || exit 1; done
 
 clean:
-	rm -f $(LIBDIR)/*.o $(LIB) $(LIB_MPI) $(LIB_TUN) $(LIB_EXP)
+	rm -f $(LIBDIR)/*.o $(LIB) $(LIB_MPI) $(LIB_TUN) $(LIBDIR)/libpdht_hip_exp*.so
 	$(MAKE) -s -C oracle clean

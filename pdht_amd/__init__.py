@@ -73,7 +73,7 @@ class _PdhtT(C.Structure):
 _lib = None        # the library the wrappers call (product, or tuning inside tuning())
 _product = None
 _tuning = None
-_exp = None  # libpdht_hip_exp.so (tools/ only)
+_exp = {}  # libpdht_hip_exp[_<tag>].so by tag (tools/ only)
 _V = C.c_void_p
 _S = C.c_size_t
 _U64 = C.c_uint64
@@ -181,16 +181,20 @@ class tuning:
     kernel variant `variant` and, optionally, `per_cu` workgroups per CU.
     The product library has no variants and no tuning entry points."""
 
-    def __init__(self, variant: int = 0, per_cu: int = 0, exp: bool = False):
+    def __init__(self, variant: int = 0, per_cu: int = 0, exp=False):
+        # exp: True = libpdht_hip_exp.so, "<tag>" = libpdht_hip_exp_<tag>.so
+        # (compile-time experiments: make exp EXP=... EXP_TAG=<tag>)
         self.variant, self.per_cu, self.exp = variant, per_cu, exp
 
     def __enter__(self):
         global _lib, _tuning, _exp
         lib()
         if self.exp:
-            if _exp is None:
-                _exp = _load(EXP_LIB_PATH, tuning=True)
-            self._t = _exp
+            tag = "" if self.exp is True else str(self.exp)
+            if tag not in _exp:
+                path = EXP_LIB_PATH if not tag else EXP_LIB_PATH.replace(".so", f"_{tag}.so")
+                _exp[tag] = _load(path, tuning=True)
+            self._t = _exp[tag]
         else:
             if _tuning is None:
                 _tuning = _load(TUNING_LIB_PATH, tuning=True)

@@ -732,13 +732,23 @@ void k_bucket_scatter_staged(
 //          chunks[g0][r] onwards, in order.
 // Both passes take their positions from the single pass's per-tile counts
 // (count kernel + scans): no extra counting and no inter-workgroup waits.
-constexpr u32 kTpCountTile = 4096;  // counting tile = pass-1 unit
+#ifndef PDHT_TP_TILE  // compile-time experiments only (make exp EXP=-DPDHT_TP_TILE=...)
+#define PDHT_TP_TILE 4096
+#endif
+#ifndef PDHT_TP_CHUNK_TILES
+#define PDHT_TP_CHUNK_TILES 8
+#endif
+#ifndef PDHT_TP_SEG_KEYS
+#define PDHT_TP_SEG_KEYS 4096
+#endif
+constexpr u32 kTpCountTile = PDHT_TP_TILE;  // counting tile = pass-1 unit
+constexpr u32 kTpSegKeys = PDHT_TP_SEG_KEYS;  // pass-2 segment: ~this many keys of one fine bucket
 // F, C <= 256.  nranks <= 8192 = 2^13: the balanced split gives F = 2^7,
 // C = 2^6; the fine-plus split of 8/16-B array outputs (late r03,
 // pdht_bucket.hip) F = 2^8 -- at this bound -- and C = 2^5.  The launcher
 // checks both before any two-pass launch.
 constexpr u32 kTpMaxDigits = 256;
-constexpr u32 kTpChunkTiles = 8;  // counting tiles per count-chunk (one count workgroup)
+constexpr u32 kTpChunkTiles = PDHT_TP_CHUNK_TILES;  // counting tiles per count-chunk (one count workgroup)
 struct TwoPass {
   u32 fbits, F, C, cbits;
   const u32 *countsF;   // [ntiles][F] fine-bucket keys of tile t before it in its 32-tile chunk

@@ -322,7 +322,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     tp.iidx = w.iidx;
     tp.ntiles = ntiles;
     tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
-    tp.SG = std::max<u64>(1, tp.F / kTpChunkTiles);  // ~4096 keys per segment
+    tp.SG = std::max<u64>(1, (u64)tp.F * kTpSegKeys / ((u64)kTpChunkTiles * kTpCountTile));  // ~kTpSegKeys keys
     tp.nsegf = (tp.nchunks + tp.SG - 1) / tp.SG;
     tp.nseg = (u64)tp.F * tp.nsegf;
   }

@@ -147,14 +147,16 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     step, result, nbytes = workload(a.work, dev)
-    # "x<N>" = variant N of the compile-time experiment build (make exp EXP=...)
+    # "x<N>" = variant N of the compile-time experiment build (make exp EXP=...),
+    # "x<N>:<tag>" = of the build made with EXP_TAG=<tag>
     combos = [(v, int(pc)) for v in a.variants.split(",") for pc in a.per_cu.split(",")]
 
     class Ctx:
         def __init__(self, v, pc):
             x = str(v).startswith("x")
-            n = int(str(v)[1:] if x else v)
-            self.c = P.tuning(n, pc, exp=True) if x else P.tuning(n, pc) if (n or pc) else None
+            vv, _, tag = str(v)[1:].partition(":") if x else (str(v), "", "")
+            n = int(vv)
+            self.c = P.tuning(n, pc, exp=tag or True) if x else P.tuning(n, pc) if (n or pc) else None
 
         def __enter__(self):
             if self.c:
