@@ -144,11 +144,11 @@ __global__ __launch_bounds__(64) void k_bucket_colscan(u32 *__restrict__ counts,
 // (a load wait also waits for older stores), then adds the sums of the waves
 // before it: one or two memory round trips instead of nchunks / 16.
 constexpr int kCsWaves = 16;
-__global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan(u32 *__restrict__ chunks, u64 nchunks,
-                                                                    u32 nranks, u64 *__restrict__ totals) {
+__device__ __forceinline__ void chunkscan_block(u32 blk, u32 *__restrict__ chunks, u64 nchunks, u32 nranks,
+                                                u64 *__restrict__ totals) {
   __shared__ u32 wsum[kCsWaves][64];
   const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const u32 r = blockIdx.x * 64 + lane;
+  const u32 r = blk * 64 + lane;
   const u64 per = (nchunks + kCsWaves - 1) / kCsWaves;
   const u64 c0 = min((u64)wave * per, nchunks), c1 = min(c0 + per, nchunks);
   constexpr u32 B = 16;
@@ -178,6 +178,22 @@ __global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan(u32 *__restr
     }
     if (wave == kCsWaves - 1) totals[r] = run;
   }
+}
+__global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan(u32 *__restrict__ chunks, u64 nchunks,
+                                                                    u32 nranks, u64 *__restrict__ totals) {
+  chunkscan_block(blockIdx.x, chunks, nchunks, nranks, totals);
+}
+// Two independent chunk scans in one launch (two-pass bucketing: the fine
+// buckets' 32-tile chunk sums and the ranks' count-chunk histograms): blocks
+// [0, nb1) scan the first, the rest the second.
+__global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan2(u32 *__restrict__ c1, u64 n1, u32 w1,
+                                                                     u64 *__restrict__ t1, u32 nb1,
+                                                                     u32 *__restrict__ c2, u64 n2, u32 w2,
+                                                                     u64 *__restrict__ t2) {
+  if (blockIdx.x < nb1)
+    chunkscan_block(blockIdx.x, c1, n1, w1, t1);
+  else
+    chunkscan_block(blockIdx.x - nb1, c2, n2, w2, t2);
 }
 
 // ------------------------------------------------------------- helpers ---
@@ -229,8 +245,14 @@ __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restr
                                                               const u64 *__restrict__ ftot,
                                                               u64 *__restrict__ fbase,
                                                               u32 *__restrict__ tickets) {
+  // the totals pass through LDS so that global loads and stores are
+  // lane-contiguous (a thread's run of consecutive ranks would make every
+  // wave instruction touch 64 lines)
+  __shared__ u64 tot[kBucketMaxRanks];
   __shared__ u64 scratch[kBaseThreads / 64];
   if (tickets && threadIdx.x < 16) tickets[threadIdx.x] = 0;  // per-XCD tile tickets of the scatter kernels
+  for (u32 r = threadIdx.x; r < nranks; r += kBaseThreads) tot[r] = totals[r];
+  __syncthreads();
   constexpr u32 kMaxPer = kBucketMaxRanks / kBaseThreads;
   const u32 per = (nranks + kBaseThreads - 1) / kBaseThreads;
   const u32 lo = min(threadIdx.x * per, nranks), hi = min(lo + per, nranks);
@@ -238,23 +260,26 @@ __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restr
   u64 s = 0;
 #pragma unroll
   for (u32 k = 0; k < kMaxPer; ++k) {
-    v[k] = lo + k < hi ? totals[lo + k] : 0;
+    v[k] = lo + k < hi ? tot[lo + k] : 0;
     s += v[k];
   }
   u64 run = block_exclusive_scan<kBaseThreads / 64, u64>(s, scratch);
 #pragma unroll
   for (u32 k = 0; k < kMaxPer; ++k)
     if (lo + k < hi) {
-      base[lo + k] = run;
-      offsets_out[lo + k] = run;
+      tot[lo + k] = run;  // each thread rewrites only its own run
       run += v[k];
     }
   if (hi == nranks && lo < hi) offsets_out[nranks] = run;
   if (nranks == 0 && threadIdx.x == 0) offsets_out[0] = 0;
+  __syncthreads();
+  for (u32 r = threadIdx.x; r < nranks; r += kBaseThreads) {
+    base[r] = tot[r];
+    offsets_out[r] = tot[r];
+  }
   if (fbase) {
     const u32 F = 1u << fbits;  // <= kTpMaxDigits
     const u64 fs = threadIdx.x < F ? ftot[threadIdx.x] : 0;
-    __syncthreads();  // scratch reuse
     const u64 fb = block_exclusive_scan<kBaseThreads / 64, u64>(fs, scratch);
     if (threadIdx.x < F) fbase[threadIdx.x] = fb;
   }

@@ -340,9 +340,9 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
                                                            ntiles);
     k_bucket_colscan<<<dim3((tp.F + 63) / 64, (unsigned)nchunks32), 64, 0, st>>>(w.countsF, ntiles, tp.F,
                                                                                    w.chunksF);
-    k_bucket_chunkscan<<<(tp.F + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunksF, nchunks32, tp.F, w.totalsF);
-    k_bucket_chunkscan<<<(nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(w.chunkcnt, tp.nchunks, nranks,
-                                                                        w.totals);
+    const u32 nbF = (tp.F + 63) / 64;  // both chunk scans in one launch
+    k_bucket_chunkscan2<<<nbF + (nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(
+        w.chunksF, nchunks32, tp.F, w.totalsF, nbF, w.chunkcnt, tp.nchunks, nranks, w.totals);
   } else if (ntiles) {
     const unsigned gc = grid_for(ntiles, 8, dev);
     if (fixed && keysize == 8)
