@@ -176,6 +176,33 @@ def plan(a, world: int) -> dict:
     return p
 
 
+# Inputs that fit the 256 MiB Infinity Cache would be re-read from it by the
+# next step (the same keys every step), not from HBM: such configs rotate
+# over copies of their keys (and bucketing over output sets too, whose
+# write-back stores could otherwise be overwritten in the cache before they
+# reach HBM), so that >= 512 MiB pass between two uses of one buffer.
+ROT_BYTES = 512 << 20
+
+
+def rot_copies(torch, t, max_copies: int = 8) -> list:
+    """t and enough identical copies that ROT_BYTES pass between two reads of
+    one of them (a buffer of >= ROT_BYTES is used alone)."""
+    nb = t.numel() * t.element_size()
+    k = min(max_copies, max(1, -(-ROT_BYTES // max(nb, 1))))
+    return [t] + [t.clone() for _ in range(k - 1)]
+
+
+def flush_infinity_cache(torch, dev):
+    """Write 512 MiB of scratch: the stores allocate in the 256 MiB Infinity
+    Cache and evict whatever the set-up left there (the freshly generated
+    keys); kernels whose loads are non-temporal never bring their inputs back,
+    so every timed step reads them from HBM."""
+    scratch = torch.empty(ROT_BYTES, dtype=torch.uint8, device=dev)
+    scratch.fill_(0x5A)
+    torch.cuda.synchronize()
+    del scratch
+
+
 def golden_folds():
     p = os.path.join(ROOT, "tests", "golden", "config_folds.json")
     if not os.path.exists(p):
@@ -226,6 +253,7 @@ def main():
     # ---------------------------------------------------------- workload ---
     keys = out = data = offs = None
     bucketed = None
+    rotation = None  # set by configs whose inputs fit the Infinity Cache (rot_copies)
     if cfg in ("records", "xrecords"):
         # f4 in the MPI wire format: one message_t record (header + key) per
         # key at its bucketed position; "xrecords" buckets by the world size
@@ -237,11 +265,16 @@ def main():
         keys = words.view(torch.uint8).view(n, L)
         nr = 1024 if cfg == "records" else world
         ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
-        recs = P.bucket_records(keys, nr, src_rank=rank, workspace=ws)
+        kset = rot_copies(torch, keys)
+        rsets = [P.bucket_records(k, nr, src_rank=rank, workspace=ws) for k in kset]
         bucketed = {"nranks": nr, "records": True}
+        turn = [0]
+        rotation = {"key_copies": len(kset), "output_sets": len(rsets)}
 
         def step():
-            rec, offs_ = P.bucket_records(keys, nr, src_rank=rank, out=recs, workspace=ws)
+            j = turn[0] % len(kset)
+            turn[0] += 1
+            rec, offs_ = P.bucket_records(kset[j], nr, src_rank=rank, out=rsets[j], workspace=ws)
             bucketed.update(rec=rec, offs=offs_)
             if cfg == "xrecords" and world > 1:
                 bucketed["x"] = D.exchange_records(rec, offs_)
@@ -263,10 +296,15 @@ def main():
         nr = {"bucket": 1024, "bucket8k": 8192}.get(cfg, world)
         bucketed = {"nranks": nr}
         ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
-        bk = P.bucket_batch(keys, 3, nr, with_ptindex=cfg != "exchange", workspace=ws)
+        kset = rot_copies(torch, keys)
+        bsets = [P.bucket_batch(k, 3, nr, with_ptindex=cfg != "exchange", workspace=ws) for k in kset]
+        turn = [0]
+        rotation = {"key_copies": len(kset), "output_sets": len(bsets)}
 
         def step():
-            ko, mb, pt, ix, offs_ = P.bucket_batch(keys, 3, nr, out=bk, workspace=ws)
+            j = turn[0] % len(kset)
+            turn[0] += 1
+            ko, mb, pt, ix, offs_ = P.bucket_batch(kset[j], 3, nr, out=bsets[j], workspace=ws)
             bucketed.update(ko=ko, mb=mb, pt=pt, ix=ix, offs=offs_)
             if cfg == "exchange" and world > 1:
                 bucketed["x"] = D.exchange_buckets(ko, mb, offs_, (ix.long() & 0xFFFFFFFF) + sh.first)
@@ -288,7 +326,18 @@ def main():
         # a 15-us launch: the step is the C call a C caller makes per batch
         # (pdht_place_batch_dev, checks and pointer lookups bound once), so
         # that the Python mirror's per-call cost does not set the step time
-        step, outs = P.bind_place_batch(keys, 1, 4, hist=hist)
+        kset = rot_copies(torch, keys)
+        calls = []
+        outs = None
+        for k in kset:
+            c, outs = P.bind_place_batch(k, 1, 4, hist=hist, out=outs)
+            calls.append(c)
+        turn = [0]
+        rotation = {"key_copies": len(kset), "output_sets": 1}
+
+        def step():
+            calls[turn[0] % len(calls)]()
+            turn[0] += 1
         out = outs[0]
         bytes_per_key = 64 + 8 + 4 + 4
         workload = f"cfg1: pdht_hash placement (mbits+ptindex+rank+hist) of {n >> 20}M x 64B keys per GPU"
@@ -328,7 +377,13 @@ def main():
             hist = torch.zeros(1024, dtype=torch.int64, device=dev)
             outs = P.place_batch(keys, 3, 1024, hist=hist)
             out = outs[0]
-            step = lambda: P.place_batch(keys, 3, 1024, hist=hist, out=outs)  # noqa: E731
+            kset = rot_copies(torch, keys)
+            turn = [0]
+            rotation = {"key_copies": len(kset), "output_sets": 1}
+
+            def step():
+                P.place_batch(kset[turn[0] % len(kset)], 3, 1024, hist=hist, out=outs)
+                turn[0] += 1
             bytes_per_key = 8 + 8 + 4 + 4
             workload = f"place: fused pdht_hash (mbits+ptindex+rank+hist) over {n >> 20}M x 8B keys per GPU"
         total_bytes_in = n * L
@@ -371,6 +426,7 @@ def main():
         step()
     kernel_name = P.last_kernel()
     torch.cuda.synchronize()
+    flush_infinity_cache(torch, dev)
     # One event pair around the K steps, on the stream the kernels are launched
     # on: the launches queue back to back as a pipelined caller's would.
     # (r01-r03 bracketed every step with its own pair; on a 15-us launch
@@ -394,7 +450,11 @@ def main():
     # checks and pointer lookups on every call) timed the same way beside it
     wrapper = None
     if cfg == "cfg1":
-        wstep = lambda: P.place_batch(keys, 1, 4, hist=hist, out=outs)  # noqa: E731
+        wturn = [0]
+
+        def wstep():
+            P.place_batch(kset[wturn[0] % len(kset)], 1, 4, hist=hist, out=outs)
+            wturn[0] += 1
         for _ in range(a.warmup):
             wstep()
         w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -488,7 +548,9 @@ def main():
         "data": "synthetic: splitmix64 key bytes (seed 0x5EED5EED5EED5EED), generated on device",
         "config": {"workload": workload, "keys_per_gpu": n, "key_bytes": L,
                    "bytes_per_key": round(bytes_per_key, 3), "kernel": kernel_name,
-                   "parallelism": f"{world} independent shards, no collective on the data path"},
+                   "parallelism": f"{world} independent shards, no collective on the data path",
+                   **({"rotation": dict(rotation, why="inputs below the 256 MiB Infinity Cache: steps cycle "
+                                        "through copies so every step reads HBM")} if rotation else {})},
         "hbm_GBps": round(achieved * world, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
@@ -515,6 +577,7 @@ def main():
         res["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds, out, P, torch)
     if "config4" in plan(a, world):
         del keys, out, words
+        kset = rsets = bsets = calls = None  # noqa: F841 (free the rotation copies)
         torch.cuda.empty_cache()
         c4 = config4_block(P, torch, D, a, rank, local, world, dev, cdev)
         if rank == 0:
@@ -545,6 +608,7 @@ def config4_block(P, torch, D, a, rank, local, world, dev, cdev) -> dict:
         P.city64_batch(keys, out=out)
     steps = max(3, a.steps // 5)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    flush_infinity_cache(torch, dev)
     torch.cuda.synchronize()
     D.barrier()
     t0 = time.perf_counter()

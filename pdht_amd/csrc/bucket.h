@@ -91,6 +91,14 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count(const uint8_t *__restri
   }
 }
 
+// Non-temporal key loads (r04, late): the bucketing steps before this one
+// left up to 256 MiB of write-back output lines in the Infinity Cache, and
+// plain (allocating) loads made this kernel evict them -- 61.8 us per 16M
+// 8-B keys against 26.9 with nt loads; the step -8.6 % (-4.6 % with the
+// outputs rotated over four sets, profiles/r04/ab/ab_bucket*_count_nt.log).
+#ifndef PDHT_COUNT_NT
+#define PDHT_COUNT_NT true
+#endif
 // Packed 8/16/32-B keys: 128 B of keys per lane loaded before any is hashed.
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_bucket_count_reg(const uint8_t *__restrict__ keys, u64 n,
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count_reg(const uint8_t *__re
     for (u64 i = k0 + threadIdx.x; i < kend; i += (u64)kBlock * U) {
       RegReader<L / 4> kr[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) load_key_regs<L, false>(keys, min(i + u * kBlock, n - 1), kr[u]);
+      for (int u = 0; u < U; ++u) load_key_regs<L, PDHT_COUNT_NT>(keys, min(i + u * kBlock, n - 1), kr[u]);
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (i + u * kBlock < kend) atomicAdd(&hist[(u32)rk.mod(city64(kr[u], (u64)L))], 1u);

@@ -16,6 +16,14 @@ constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wa
 // r01 interleaved A/B (profiles/r01/placebench_*): 8-B keys with non-temporal
 // stores (+26 % on fused placement), 16-B keys with non-temporal loads and
 // stores (+6-11 %).
+// 8-B placement with a histogram loads its keys non-temporally (r04, late):
+// with the keys rotated over buffers larger than the Infinity Cache (bench.py
+// rot_copies) 0.605 -> 0.640 of the roofline; r01's plain-load choice was
+// measured re-reading one cache-resident 128 MiB key buffer
+// (profiles/r04/ab/ab_place*_nt.log).
+#ifndef PDHT_PLACE8_NT
+#define PDHT_PLACE8_NT true
+#endif
 template <class Algo, class Sink>
 static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Sink sink,
                          hipStream_t st, int dev, u64 blocks) {
@@ -32,8 +40,8 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // workgroup per CU -- 0.80 of the roofline against 0.74 at two, half the
     // flushes again; 16-B keys stay at two)
     if (sink.hist && keylen == 8) {
-      g_kernel = "k_fixed_direct<8,4,nt-store,1024>@1";
-      k_fixed_direct<8, 4, Algo, SinkNt, false, 1024>
+      g_kernel = "k_fixed_direct<8,4,nt,1024>@1";
+      k_fixed_direct<8, 4, Algo, SinkNt, PDHT_PLACE8_NT, 1024>
           <<<grid_for((blocks + 15) / 16, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
       return;
     }

@@ -85,6 +85,81 @@ def workload(name, dev):
             return (lambda: P.city128_batch(keys, out=out)), (lambda: out.clone()), n * (L + 16)
         return ((lambda: P.city128_seed_batch(keys, (0x0123456789ABCDEF, 0xFEDCBA9876543210), out=out)),
                 (lambda: out.clone()), n * (L + 16))
+    if name == "placerot":
+        # place (16M x 8 B, nptes 3, 1024 ranks, histogram) with the KEYS
+        # rotated over 4 sets (512 MiB): no step finds its keys still in the
+        # Infinity Cache from the step before
+        n = 16 * M
+        ks = [P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8) for _ in range(4)]
+        hist = torch.zeros(1024, dtype=torch.int64, device=dev)
+        outs = P.place_batch(ks[0], 3, 1024)
+        turn = [0]
+
+        def step():
+            P.place_batch(ks[turn[0] % 4], 3, 1024, hist=hist, out=outs)
+            turn[0] += 1
+        return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 24
+    if name in ("bucketrot", "recordsrot"):
+        # bucket / records at 1024 ranks with the outputs rotated over 4 sets
+        # (1.5 GiB): no output line can still sit in the Infinity Cache when
+        # its address is written again (what reusing one set could hide)
+        n = 16 * M
+        keys = P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8)
+        with P.tuning(0):  # the tuning / experiment builds reserve the two-pass intermediate too
+            wsb = P.bucket_workspace_bytes(n, 8, 1024)
+        ws = torch.empty(max(wsb, P.bucket_workspace_bytes(n, 8, 1024)), dtype=torch.uint8, device=dev)
+        if name == "recordsrot":
+            sets = [P.bucket_records(keys, 1024, workspace=ws) for _ in range(4)]
+        else:
+            sets = [P.bucket_batch(keys, 3, 1024, workspace=ws) for _ in range(4)]
+        turn = [0]
+
+        def step():
+            o = sets[turn[0] % 4]
+            turn[0] += 1
+            if name == "recordsrot":
+                P.bucket_records(keys, 1024, out=o, workspace=ws)
+            else:
+                P.bucket_batch(keys, 3, 1024, out=o, workspace=ws)
+        if name == "recordsrot":
+            return step, (lambda: torch.cat([sets[0][0].view(-1)[:1 << 20].long(), sets[0][1]])), n * 40
+        return step, (lambda: torch.cat([sets[0][1], sets[0][3].long(), sets[0][4]])), n * 32
+    if name in ("bucketpg", "bucketpg64k", "bucketwarm"):
+        # before each bucketing step, touch the keys: one byte per 4 KiB page
+        # (pg) / per 64 KiB (pg64k) -- translations warm, data not -- or read
+        # them all (warm: translations and the Infinity Cache both warm)
+        n = 16 * M
+        keys = P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8)
+        ws = torch.empty(P.bucket_workspace_bytes(n, 8, 1024), dtype=torch.uint8, device=dev)
+        outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
+        flat = keys.view(-1)
+        gout = torch.zeros(1, dtype=torch.int64, device=dev)
+        st = 4096 if name == "bucketpg" else 65536
+
+        def step():
+            if name == "bucketwarm":
+                P.read_stream(flat, True, out=gout)
+            else:
+                gout.copy_(flat[::st].to(torch.int64).sum().view(1))
+            P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)
+        return step, (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * 32
+    if name in ("bucketgap", "gaponly"):
+        # diagnostics of the count kernel's "drain" (DESIGN.md §4.4): bucketing
+        # steps with a 1 GiB read-only stream between them (bucketgap), and that
+        # stream alone (gaponly); rocprof tells the kernels apart
+        n = 16 * M
+        gap = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        gout = torch.zeros(1, dtype=torch.int64, device=dev)
+        if name == "gaponly":
+            return (lambda: P.read_stream(gap, True, out=gout)), (lambda: gout.clone()), 1 << 30
+        keys = P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8)
+        ws = torch.empty(P.bucket_workspace_bytes(n, 8, 1024), dtype=torch.uint8, device=dev)
+        outs = P.bucket_batch(keys, 3, 1024, workspace=ws)
+
+        def step():
+            P.bucket_batch(keys, 3, 1024, out=outs, workspace=ws)
+            P.read_stream(gap, True, out=gout)
+        return step, (lambda: torch.cat([outs[1], outs[3].long(), outs[4]])), n * 32 + (1 << 30)
     if name in ("cfg2", "cfg5", "cfg4", "long", "long64", "place", "bucket"):
         L = {"cfg2": 64, "cfg5": 64, "cfg4": 64, "long": 1024, "long64": 1024, "place": 8, "bucket": 8}[name]
         n = M if name in ("long", "long64") else 128 * M if name == "cfg5" else 16 * M

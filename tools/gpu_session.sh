@@ -50,6 +50,10 @@ for step in "$@"; do
     sq_*)    cfg=${step#sq_}
              timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sq_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/sq_$cfg.log 2>&1; rc=$?
              tail -3 gpurun_out/sq_$cfg.log | cut -c1-300 ;;
+    profab_*) w=${step#profab_}; d="gpurun_out/$step"
+             # rocprof kernel stats of the A/B harness's workload (product only)
+             timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$d" -o run --output-format csv -- python3 tools/abbench.py --work $w --variants ${VARIANTS:-0} --rounds ${ROUNDS:-3} --reps ${REPS:-10} ${PAIR:+--pair} > "$d.log" 2>&1; rc=$?
+             python3 -c "import csv,sys; [print(r['Name'][:90], r['Calls'], r['AverageNs'], r['MinNs'], r['MaxNs']) for r in csv.DictReader(open(sys.argv[1])) if 'pdht' in r['Name']]" "$d/run_kernel_stats.csv" ;;
     sqab_*)  w=${step#sqab_}
              # SQ counters of the A/B harness's variants (one rocprofv3 pass; kernels told apart by name)
              timeout -s KILL 200 rocprofv3 --pmc ${PMCS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS} --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sqab_$w" -o run --output-format csv -- python3 tools/abbench.py --work $w --variants ${VARIANTS:-0} --rounds 1 --reps 3 > gpurun_out/sqab_$w.log 2>&1; rc=$?
