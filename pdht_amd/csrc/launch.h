@@ -39,10 +39,27 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // (r02, tools/abbench.py place8_*: 8-B keys stream best at ONE such
     // workgroup per CU -- 0.80 of the roofline against 0.74 at two, half the
     // flushes again; 16-B keys stay at two)
+#ifdef PDHT_HIP_TUNING
+    if (sink.hist && keylen == 8 && (tuning_variant() == 219 || tuning_variant() == 220)) {
+      // r04: 4 (the shape before) / 16 keys per lane in flight
+      if (tuning_variant() == 219) {
+        g_kernel = "k_fixed_direct<8,4,nt,1024>@1";
+        k_fixed_direct<8, 4, Algo, SinkNt, true, 1024>
+            <<<grid_for((blocks + 15) / 16, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
+      } else {
+        g_kernel = "k_fixed_direct<8,16,nt,1024>@1";
+        k_fixed_direct<8, 16, Algo, SinkNt, true, 1024>
+            <<<grid_for((blocks + 63) / 64, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
+      }
+      return;
+    }
+#endif
+    // 8 keys per lane in flight (late r04, HBM-resident keys: 0.621 -> 0.681
+    // against 4; 16: 0.629; profiles/r04/ab/ab_placerot_shapes.log)
     if (sink.hist && keylen == 8) {
-      g_kernel = "k_fixed_direct<8,4,nt,1024>@1";
-      k_fixed_direct<8, 4, Algo, SinkNt, PDHT_PLACE8_NT, 1024>
-          <<<grid_for((blocks + 15) / 16, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
+      g_kernel = "k_fixed_direct<8,8,nt,1024>@1";
+      k_fixed_direct<8, 8, Algo, SinkNt, PDHT_PLACE8_NT, 1024>
+          <<<grid_for((blocks + 31) / 32, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
       return;
     }
     if (sink.hist && keylen == 16) {
@@ -52,18 +69,50 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
       return;
     }
   }
+#ifdef PDHT_HIP_TUNING
+  if (keylen == 8 && tuning_variant() >= 221 && tuning_variant() <= 223) {
+    // r04: plain loads (221, the shape before), 8 keys per lane (222; 223 as 1024-thread @1)
+    if (tuning_variant() == 221) {
+      g_kernel = "k_fixed_direct<8,4,nt-store>@8";
+      k_fixed_direct<8, 4, Algo, SinkNt, false><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                                      snt);
+    } else if (tuning_variant() == 222) {
+      g_kernel = "k_fixed_direct<8,8,nt>@8";
+      k_fixed_direct<8, 8, Algo, SinkNt, true><<<grid_for((blocks + 7) / 8, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                                     snt);
+    } else {
+      g_kernel = "k_fixed_direct<8,8,nt,1024>@1";
+      k_fixed_direct<8, 8, Algo, SinkNt, true, 1024>
+          <<<grid_for((blocks + 31) / 32, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
+    }
+    return;
+  }
+#endif
   if (keylen == 8) {
-    g_kernel = "k_fixed_direct<8,4,nt-store>@8";
-    k_fixed_direct<8, 4, Algo, SinkNt, false><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(
+    // non-temporal loads since late r04: 0.659 -> 0.712 with HBM-resident
+    // keys (r01's plain loads were chosen on a cache-resident buffer;
+    // profiles/r04/ab/ab_city8rot.log)
+    g_kernel = "k_fixed_direct<8,4,nt>@8";
+    k_fixed_direct<8, 4, Algo, SinkNt, true><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(
         k, n, algo, snt);
   } else if (keylen == 16) {
     g_kernel = "k_fixed_direct<16,2,nt>@8";
     k_fixed_direct<16, 2, Algo, SinkNt, true><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(
         k, n, algo, snt);
   } else {
-    g_kernel = "k_fixed_direct<32,2>@8";
-    k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo,
-                                                                                            sink);
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 224) {  // plain loads and stores for 32-B keys (the shape before late r04)
+      g_kernel = "k_fixed_direct<32,2>@8";
+      k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                              sink);
+      return;
+    }
+#endif
+    // non-temporal loads and stores since late r04: 0.628 -> 0.688 with
+    // HBM-resident keys (profiles/r04/ab/ab_city32rot.log)
+    g_kernel = "k_fixed_direct<32,2,nt>@8";
+    k_fixed_direct<32, 2, Algo, SinkNt, true><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                                    snt);
   }
 }
 

@@ -55,8 +55,8 @@ def test_generator_matches_oracle(dev, oracle):
     assert (lens.cpu().numpy().astype(np.uint64) == oracle.mixed_lengths(5000)).all()
 
 
-SMALL_KERNELS = {8: "k_fixed_direct<8,4,nt-store>@8", 16: "k_fixed_direct<16,2,nt>@8",
-                 32: "k_fixed_direct<32,2>@8", 64: "k_fixed_xpose64<nt,d2>@3"}
+SMALL_KERNELS = {8: "k_fixed_direct<8,4,nt>@8", 16: "k_fixed_direct<16,2,nt>@8",
+                 32: "k_fixed_direct<32,2,nt>@8", 64: "k_fixed_xpose64<nt,d2>@3"}
 
 
 def fixed_kernel(L, stride=None, aligned=True, crc=False):

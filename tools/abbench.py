@@ -85,6 +85,30 @@ def workload(name, dev):
             return (lambda: P.city128_batch(keys, out=out)), (lambda: out.clone()), n * (L + 16)
         return ((lambda: P.city128_seed_batch(keys, (0x0123456789ABCDEF, 0xFEDCBA9876543210), out=out)),
                 (lambda: out.clone()), n * (L + 16))
+    if name in ("city8rot", "city32rot"):
+        # CityHash64 of 16M x 8-B / 32-B keys (no placement), keys rotated over 4 copies
+        n, L = 16 * M, (8 if name == "city8rot" else 32)
+        ks = [P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L) for _ in range(4)]
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        turn = [0]
+
+        def step():
+            P.city64_batch(ks[turn[0] % 4], out=out)
+            turn[0] += 1
+        return step, (lambda: out.clone()), n * (L + 8)
+    if name == "cfg1rot":
+        # cfg1 (1M x 64 B, nptes 1, 4 ranks, histogram) with the keys rotated
+        # over 8 copies (512 MiB), as bench.py measures it
+        n, L = M, 64
+        ks = [P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L) for _ in range(8)]
+        hist = torch.zeros(4, dtype=torch.int64, device=dev)
+        outs = P.place_batch(ks[0], 1, 4, hist=hist)
+        turn = [0]
+
+        def step():
+            P.place_batch(ks[turn[0] % 8], 1, 4, hist=hist, out=outs)
+            turn[0] += 1
+        return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 80
     if name == "placerot":
         # place (16M x 8 B, nptes 3, 1024 ranks, histogram) with the KEYS
         # rotated over 4 sets (512 MiB): no step finds its keys still in the
