@@ -68,6 +68,11 @@ extern "C" {
  *                     F = 2^ceil(nbits/2) (product: one fine bit more)
  *   records      112  r02 store order (header halves a staging round early)
  *   host          61  chunked copy pipeline instead of zero-copy on pinned buffers
+ *   small keys   219  8-B placement with a histogram, 4 keys per lane (the shape
+ *                     before late r04; product: 8); 220 16 keys per lane
+ *            221-223  8-B hashing: plain loads (the shape before late r04; product:
+ *                     non-temporal) / 8 keys per lane / 8 keys per lane, 1024 threads @1
+ *                224  32-B keys with plain loads and stores (product: non-temporal)
  * Process-wide; returns the previous value. */
 int pdht_hip_set_variant(int variant);
 /* Override the workgroups per CU of the persistent grids (0 = default).
