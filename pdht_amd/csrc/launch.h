@@ -62,6 +62,14 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
           <<<grid_for((blocks + 31) / 32, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
       return;
     }
+#ifdef PDHT_HIP_TUNING
+    if (sink.hist && keylen == 16 && tuning_variant() == 225) {  // r04: 4 keys per lane in flight
+      g_kernel = "k_fixed_direct<16,4,nt,1024>@2";
+      k_fixed_direct<16, 4, Algo, SinkNt, true, 1024>
+          <<<grid_for((blocks + 15) / 16, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
+      return;
+    }
+#endif
     if (sink.hist && keylen == 16) {
       g_kernel = "k_fixed_direct<16,2,nt,1024>@2";
       k_fixed_direct<16, 2, Algo, SinkNt, true, 1024>
@@ -96,6 +104,14 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     k_fixed_direct<8, 4, Algo, SinkNt, true><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(
         k, n, algo, snt);
   } else if (keylen == 16) {
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 226) {  // r04: 4 keys per lane in flight
+      g_kernel = "k_fixed_direct<16,4,nt>@8";
+      k_fixed_direct<16, 4, Algo, SinkNt, true><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo,
+                                                                                                      snt);
+      return;
+    }
+#endif
     g_kernel = "k_fixed_direct<16,2,nt>@8";
     k_fixed_direct<16, 2, Algo, SinkNt, true><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(
         k, n, algo, snt);

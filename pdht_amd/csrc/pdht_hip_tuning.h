@@ -73,6 +73,8 @@ extern "C" {
  *            221-223  8-B hashing: plain loads (the shape before late r04; product:
  *                     non-temporal) / 8 keys per lane / 8 keys per lane, 1024 threads @1
  *                224  32-B keys with plain loads and stores (product: non-temporal)
+ *           225, 226  16-B keys, 4 keys per lane in flight: placement with a histogram
+ *                     (1024 threads @2) / hashing (@8) (product: 2)
  * Process-wide; returns the previous value. */
 int pdht_hip_set_variant(int variant);
 /* Override the workgroups per CU of the persistent grids (0 = default).

@@ -85,9 +85,9 @@ def workload(name, dev):
             return (lambda: P.city128_batch(keys, out=out)), (lambda: out.clone()), n * (L + 16)
         return ((lambda: P.city128_seed_batch(keys, (0x0123456789ABCDEF, 0xFEDCBA9876543210), out=out)),
                 (lambda: out.clone()), n * (L + 16))
-    if name in ("city8rot", "city32rot"):
-        # CityHash64 of 16M x 8-B / 32-B keys (no placement), keys rotated over 4 copies
-        n, L = 16 * M, (8 if name == "city8rot" else 32)
+    if name in ("city8rot", "city16rot", "city32rot"):
+        # CityHash64 of 16M x 8/16/32-B keys (no placement), keys rotated over 4 copies
+        n, L = 16 * M, int(name[4:-3])
         ks = [P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L) for _ in range(4)]
         out = torch.empty(n, dtype=torch.int64, device=dev)
         turn = [0]
@@ -109,12 +109,12 @@ def workload(name, dev):
             P.place_batch(ks[turn[0] % 8], 1, 4, hist=hist, out=outs)
             turn[0] += 1
         return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 80
-    if name == "placerot":
-        # place (16M x 8 B, nptes 3, 1024 ranks, histogram) with the KEYS
-        # rotated over 4 sets (512 MiB): no step finds its keys still in the
+    if name in ("placerot", "place16rot"):
+        # place (16M x 8 / 16 B, nptes 3, 1024 ranks, histogram) with the KEYS
+        # rotated over 4 sets (>= 512 MiB): no step finds its keys still in the
         # Infinity Cache from the step before
-        n = 16 * M
-        ks = [P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8) for _ in range(4)]
+        n, L = 16 * M, (8 if name == "placerot" else 16)
+        ks = [P.splitmix64_fill(SEED, 0, n * L // 8, device=dev).view(torch.uint8).view(n, L) for _ in range(4)]
         hist = torch.zeros(1024, dtype=torch.int64, device=dev)
         outs = P.place_batch(ks[0], 3, 1024)
         turn = [0]
@@ -122,7 +122,7 @@ def workload(name, dev):
         def step():
             P.place_batch(ks[turn[0] % 4], 3, 1024, hist=hist, out=outs)
             turn[0] += 1
-        return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * 24
+        return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * (L + 16)
     if name in ("bucketrot", "recordsrot"):
         # bucket / records at 1024 ranks with the outputs rotated over 4 sets
         # (1.5 GiB): no output line can still sit in the Infinity Cache when
