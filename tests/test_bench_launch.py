@@ -103,3 +103,31 @@ def test_world_size_mismatch_is_an_error():
     assert p.returncode != 0
     assert "WORLD_SIZE=3" in p.stderr
     assert _json_lines(p.stdout) == []
+
+
+def test_cache_sized_inputs_rotate_past_the_infinity_cache():
+    """Inputs that fit the 256 MiB Infinity Cache are cycled through enough
+    identical copies that >= 512 MiB pass between two reads of one copy
+    (bench.rot_copies); larger inputs are used alone."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class T:  # stands in for a tensor: size and clone only
+        def __init__(self, nbytes):
+            self.nbytes = nbytes
+
+        def numel(self):
+            return self.nbytes
+
+        def element_size(self):
+            return 1
+
+        def clone(self):
+            return T(self.nbytes)
+
+    M = 1 << 20
+    for nbytes, copies in ((64 * M, 8), (128 * M, 4), (256 * M, 2), (1 << 30, 1), (8 << 30, 1), (1 * M, 8)):
+        ks = bench.rot_copies(None, T(nbytes))
+        assert len(ks) == copies
+        assert all(k.nbytes == nbytes for k in ks)
+        assert copies == 8 or copies * nbytes >= bench.ROT_BYTES
