@@ -123,28 +123,30 @@ def workload(name, dev):
             P.place_batch(ks[turn[0] % 4], 3, 1024, hist=hist, out=outs)
             turn[0] += 1
         return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * (L + 16)
-    if name in ("bucketrot", "recordsrot"):
-        # bucket / records at 1024 ranks with the outputs rotated over 4 sets
-        # (1.5 GiB): no output line can still sit in the Infinity Cache when
-        # its address is written again (what reusing one set could hide)
+    if name in ("bucketrot", "recordsrot", "bucket8krot"):
+        # bucket / records at 1024 ranks (bucket8k: 8192 ranks, two passes)
+        # with the keys rotated over 4 copies and the outputs over 4 sets, as
+        # bench.py measures them: no output line can still sit in the
+        # Infinity Cache when its address is written again
         n = 16 * M
-        keys = P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8)
+        nr = 8192 if name == "bucket8krot" else 1024
+        kk = [P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8) for _ in range(4)]
         with P.tuning(0):  # the tuning / experiment builds reserve the two-pass intermediate too
-            wsb = P.bucket_workspace_bytes(n, 8, 1024)
-        ws = torch.empty(max(wsb, P.bucket_workspace_bytes(n, 8, 1024)), dtype=torch.uint8, device=dev)
+            wsb = P.bucket_workspace_bytes(n, 8, nr)
+        ws = torch.empty(max(wsb, P.bucket_workspace_bytes(n, 8, nr)), dtype=torch.uint8, device=dev)
         if name == "recordsrot":
-            sets = [P.bucket_records(keys, 1024, workspace=ws) for _ in range(4)]
+            sets = [P.bucket_records(k, nr, workspace=ws) for k in kk]
         else:
-            sets = [P.bucket_batch(keys, 3, 1024, workspace=ws) for _ in range(4)]
+            sets = [P.bucket_batch(k, 3, nr, workspace=ws) for k in kk]
         turn = [0]
 
         def step():
-            o = sets[turn[0] % 4]
+            j = turn[0] % 4
             turn[0] += 1
             if name == "recordsrot":
-                P.bucket_records(keys, 1024, out=o, workspace=ws)
+                P.bucket_records(kk[j], nr, out=sets[j], workspace=ws)
             else:
-                P.bucket_batch(keys, 3, 1024, out=o, workspace=ws)
+                P.bucket_batch(kk[j], 3, nr, out=sets[j], workspace=ws)
         if name == "recordsrot":
             return step, (lambda: torch.cat([sets[0][0].view(-1)[:1 << 20].long(), sets[0][1]])), n * 40
         return step, (lambda: torch.cat([sets[0][1], sets[0][3].long(), sets[0][4]])), n * 32
