@@ -15,12 +15,12 @@ constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wa
 // so 8- and 16-byte keys are fully coalesced), U keys in flight per lane.
 // r01 interleaved A/B (profiles/r01/placebench_*): 8-B keys with non-temporal
 // stores (+26 % on fused placement), 16-B keys with non-temporal loads and
-// stores (+6-11 %).
-// 8-B placement with a histogram loads its keys non-temporally (r04, late):
-// with the keys rotated over buffers larger than the Infinity Cache (bench.py
-// rot_copies) 0.605 -> 0.640 of the roofline; r01's plain-load choice was
-// measured re-reading one cache-resident 128 MiB key buffer
-// (profiles/r04/ab/ab_place*_nt.log).
+// stores (+6-11 %).  Late r04 re-measured the shapes with the keys rotated
+// over buffers larger than the 256 MiB Infinity Cache (bench.py rot_copies;
+// r01 had re-read one cache-resident key buffer): every width now loads
+// non-temporally -- 8-B placement 0.605 -> 0.640, 8-B hashing 0.659 -> 0.712,
+// 32-B 0.628 -> 0.688 (with nt stores) -- and 8-B placement keeps 8 keys per
+// lane in flight (0.621 -> 0.681) (profiles/r04/ab/*rot*.log).
 #ifndef PDHT_PLACE8_NT
 #define PDHT_PLACE8_NT true
 #endif
