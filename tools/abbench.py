@@ -11,7 +11,13 @@ stream; every variant's output is compared with the product kernel's.
          varfold_<L> (64M x L-B fixed keys through the var calibration entry),
          long (1M x 1 KiB Crc128), long64 (1M x 1 KiB City64),
          place (16M x 8 B, nptes 3, nranks 1024, histogram),
-         bucket (16M x 8 B, 1024 ranks, keys+mbits+ptindex+index)
+         bucket (16M x 8 B, 1024 ranks, keys+mbits+ptindex+index),
+         bucket_<L>_<nranks> / records_<L>_<nranks>, place<L>_<nranks>, cfg1 / cfg1nohist;
+         with inputs rotated past the 256 MiB Infinity Cache (as bench.py measures):
+         cfg1rot, placerot, place16rot, city8rot / city16rot / city32rot,
+         bucketrot, recordsrot, bucket8krot (outputs rotated too);
+         diagnostics of the bucketing count kernel: bucketgap, gaponly,
+         bucketpg, bucketpg64k, bucketwarm
 Variant 0 runs through the PRODUCT library; the others through the tuning
 build (pdht_amd.tuning).  Numbers: median / min ms and algorithmic GB/s.
 """
