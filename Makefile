@@ -13,7 +13,9 @@
 
 HIPCC   ?= /opt/rocm/bin/hipcc
 CC      ?= gcc
-ARCH    ?= gfx950
+# gfx950 only: the kernels size their LDS for its 160 KiB per CU (e.g.
+# k_bucket_base stages 64 KiB of totals), which other targets do not have
+ARCH    := gfx950
 LIBDIR  := pdht_amd/lib
 LIB     := $(LIBDIR)/libpdht_hip.so
 LIB_MPI := $(LIBDIR)/libpdht_hip_mpi.so
@@ -23,6 +25,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
 CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
 HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/runtime.h \
+           pdht_amd/csrc/bucket.h pdht_amd/csrc/launch.h \
            pdht_amd/csrc/pdht_hip_tuning.h include/pdht_hip.h include/pdht_city.h
 SHIM_HDR := include/pdht_hash.h include/pdht_hip.h include/pdht_city.h
 # the C-ABI in translation units that build in parallel (make -j)
@@ -35,7 +38,7 @@ OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
 
 # Compile-time experiments for tools/abbench.py (`--variants x0` = variant 0
 # of this build): the tuning build plus EXP flags, e.g.
-#   make exp EXP=-DPDHT_MUL_MAD [EXP_TAG=mad -> libpdht_hip_exp_mad.so, `--variants x0:mad`]
+#   make exp EXP=-DPDHT_COUNT_NT=false [EXP_TAG=cnt -> libpdht_hip_exp_cnt.so, `--variants x0:cnt`]
 EXP ?=
 EXP_TAG ?=
 LIB_EXP := $(LIBDIR)/libpdht_hip_exp$(if $(EXP_TAG),_$(EXP_TAG)).so

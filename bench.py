@@ -76,16 +76,21 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg1", "cfg2", "cfg2r", "cfg3", "cfg4", "cfg5", "place", "bucket", "bucket8k", "exchange",
-                             "records", "xrecords", "long"])
+                    choices=["cfg1", "cfg2", "cfg2r", "cfg3", "cfg4", "cfg5", "config4", "place", "bucket", "bucket8k",
+                             "exchange", "records", "xrecords", "long"],
+                    help="workload of the line (default cfg2 = BASELINE configs[1]); config4 = BASELINE configs[4] "
+                         "alone as the line's workload: the 1B x 64 B stream split over the N ranks (strong "
+                         "scaling), without the cfg2 leg -- what a profile of configs[4] alone runs")
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override the per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.5,
                     help="wall budget of one CPU-baseline pass (best of 5 passes)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="collective backend at N > 1: nccl (= RCCL, one GPU per rank) or gloo (a rehearsal: "
-                         "ranks share the visible GPUs round-robin, collectives on CPU tensors)")
+    ap.add_argument("--dist-backend", default=None, choices=["nccl", "gloo"],
+                    help="collective backend: nccl (= RCCL, one GPU per rank; the default at N > 1) or gloo (a "
+                         "rehearsal: ranks share the visible GPUs round-robin, collectives on CPU tensors).  "
+                         "Given at N = 1, the one rank still joins a process group of that backend, so the "
+                         "collectives (and the exchange of the exchange/xrecords configs) run through it")
     ap.add_argument("--no-config4", action="store_true",
                     help="skip the BASELINE configs[4] block (1B x 64 B keys split over the N ranks)")
     ap.add_argument("--dry-run", action="store_true",
@@ -230,19 +235,30 @@ def main():
     from pdht_amd import dist as D
 
     rank, local, world = D.env_rank_world()
-    if world > 1 and a.dist_backend == "gloo":
+    backend = a.dist_backend or ("nccl" if world > 1 else None)
+    if world == 1 and backend is not None:
+        # one rank in a group of one: every collective of the N-rank path
+        # (barrier, max of times, parity reductions, per-rank gathers and the
+        # exchange's all-to-all(v)) runs through the backend -- on one GPU box
+        # the only way to execute the RCCL path on device tensors
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if backend == "gloo":
         # rehearsal of the N-rank path on fewer GPUs (e.g. 2 ranks on the one
         # GPU of a gpurun box, where RCCL refuses two ranks per device): ranks
         # share devices round-robin, the collectives run on CPU tensors
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group("gloo")
-    elif world > 1:
+    elif backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+    a.dist_backend = backend
     dev = torch.device("cuda", torch.cuda.current_device())
-    cdev = dev if world > 1 and a.dist_backend == "nccl" else None  # where the collectives' tensors live
+    cdev = dev if backend == "nccl" else None  # where the collectives' tensors live
 
     if not os.path.exists(os.path.join(ROOT, "pdht_amd", "lib", "libpdht_hip.so")):
         import __graft_entry__
@@ -276,7 +292,7 @@ def main():
             turn[0] += 1
             rec, offs_ = P.bucket_records(kset[j], nr, src_rank=rank, out=rsets[j], workspace=ws)
             bucketed.update(rec=rec, offs=offs_)
-            if cfg == "xrecords" and world > 1:
+            if cfg == "xrecords" and dist.is_initialized():
                 bucketed["x"] = D.exchange_records(rec, offs_)
         out = None
         bytes_per_key = L + P.bucket_record_bytes(L)
@@ -306,7 +322,7 @@ def main():
             turn[0] += 1
             ko, mb, pt, ix, offs_ = P.bucket_batch(kset[j], 3, nr, out=bsets[j], workspace=ws)
             bucketed.update(ko=ko, mb=mb, pt=pt, ix=ix, offs=offs_)
-            if cfg == "exchange" and world > 1:
+            if cfg == "exchange" and dist.is_initialized():
                 bucketed["x"] = D.exchange_buckets(ko, mb, offs_, (ix.long() & 0xFFFFFFFF) + sh.first)
         out = None
         bytes_per_key = L + L + 8 + 4 + (4 if cfg != "exchange" else 0)
@@ -342,10 +358,13 @@ def main():
         bytes_per_key = 64 + 8 + 4 + 4
         workload = f"cfg1: pdht_hash placement (mbits+ptindex+rank+hist) of {n >> 20}M x 64B keys per GPU"
         total_bytes_in = n * L
-    elif cfg in ("cfg2", "cfg2r", "cfg4", "cfg5", "place"):
+    elif cfg in ("cfg2", "cfg2r", "cfg4", "cfg5", "config4", "place"):
         L = 8 if cfg == "place" else 64
         n = a.keys_per_gpu or (128 * M if cfg == "cfg5" else 16 * M)
         sh = D.weak_shard(rank, world, n)
+        if cfg == "config4":  # the 1B keys split over the ranks (strong scaling)
+            sh = D.strong_shard(rank, world, CONFIG4_KEYS)
+            n = sh.n
         words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
         if cfg == "cfg2r":
@@ -362,12 +381,13 @@ def main():
             bytes_per_key = 64 + 8
             workload = (f"cfg2r: CityHash64 over {n >> 20}M x 64B keys per GPU, device-resident, digests written "
                         f"round-robin into 4 buffers (every step's digests reach HBM)")
-        elif cfg in ("cfg2", "cfg5"):
+        elif cfg in ("cfg2", "cfg5", "config4"):
             out = torch.empty(n, dtype=torch.int64, device=dev)
             step = lambda: P.city64_batch(keys, out=out)  # noqa: E731
             bytes_per_key = 64 + 8
             workload = (f"{cfg}: CityHash64 over {n >> 20}M x 64B keys per GPU, device-resident"
-                        + (" (BASELINE configs[4] = 1B keys at N=8)" if cfg == "cfg5" else ""))
+                        + (" (BASELINE configs[4] = 1B keys at N=8)" if cfg == "cfg5" else "")
+                        + (f" (BASELINE configs[4]: 1B keys split over {world} GPU(s))" if cfg == "config4" else ""))
         elif cfg == "cfg4":
             out = torch.empty((n, 2), dtype=torch.int64, device=dev)
             step = lambda: P.citycrc128_batch(keys, out=out)  # noqa: E731
@@ -486,7 +506,7 @@ def main():
         calib = round(keys.numel() / (cms / 1e3) / 1e9, 1)
     # the 64-B kernel's own data movement with the hash replaced by an XOR fold
     calib_key = None
-    if cfg in ("cfg2", "cfg2r", "cfg5"):
+    if cfg in ("cfg2", "cfg2r", "cfg5", "config4"):
         fold = torch.empty(n, dtype=torch.int64, device=dev)
         P.key_stream(keys, out=fold)
         cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -531,10 +551,10 @@ def main():
             parity = check_parity(P, torch, D, cfg, sh, out, extra, cdev)
 
     # ------------------------------------------------------- report ------
-    value = n * world * a.steps / elapsed_max / 1e9
+    value = (CONFIG4_KEYS if cfg == "config4" else n * world) * a.steps / elapsed_max / 1e9
     achieved = bytes_per_key * n / (kern_ms / 1e3) / 1e9
     res = {
-        "metric": METRIC if cfg in ("cfg2", "cfg5", "cfg2r") else f"{cfg}: Gkeys/s and achieved HBM GB/s",
+        "metric": METRIC if cfg in ("cfg2", "cfg5", "cfg2r", "config4") else f"{cfg}: Gkeys/s and achieved HBM GB/s",
         "value": round(value, 4),
         "unit": "Gkeys/s",
         "n_gpus": world,
@@ -542,7 +562,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if cfg == "config4" else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic: splitmix64 key bytes (seed 0x5EED5EED5EED5EED), generated on device",
@@ -566,7 +586,7 @@ def main():
     }
     if wrapper is not None:
         res["cfg1_wrapper_path"] = wrapper
-    if world > 1:
+    if world > 1 or dist.is_initialized():
         res["per_rank"] = D.per_rank_report(rank, local, world, n, bytes_per_key, kern_ms, elapsed, a.steps,
                                             PEAK_HBM_GBPS, device=dev)
     if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:  # (cfg2r: the same host path as cfg2)
@@ -582,12 +602,14 @@ def main():
         c4 = config4_block(P, torch, D, a, rank, local, world, dev, cdev)
         if rank == 0:
             res["baseline_config4"] = c4
-            w4 = parity_word(c4["parity"])
-            if w4 != "ok" and parity_word(res["parity"]) == "ok":  # the line says the worst of both
+            # the line leads with the worse of the two words (FAILED < unchecked < ok)
+            order = list(PAR_WORD.values())
+            w4, w0 = parity_word(c4["parity"]), parity_word(res["parity"])
+            if order.index(w4) < order.index(w0):
                 res["parity"] = f"{w4}: " + res["parity"] + " | configs[4] block: " + c4["parity"]
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -679,7 +701,7 @@ def golden_shard_fold(folds, cfg, sh):
     """Reference fold of exactly this shard's keys, when the golden file has it."""
     if folds is None:
         return None, None
-    if cfg in ("cfg2", "cfg5"):
+    if cfg in ("cfg2", "cfg5", "config4"):
         f = city64_chunk_fold(folds, sh.first, sh.n)
         if f is not None:
             return f, f"cfg5 16M-key chunks {sh.first // (16 * M)}..{(sh.first + sh.n) // (16 * M) - 1}"
@@ -963,7 +985,7 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
         s_n, mode, nptes, nranks = M, 2, 1, 4
         data = O.fixed_keys(s_n, 64)
         what = "all 1M x 64B keys of cfg1, per-key pdht_hash semantics (nptes 1, nranks 4)"
-    elif cfg in ("cfg2", "cfg2r", "cfg5"):
+    elif cfg in ("cfg2", "cfg2r", "cfg5", "config4"):
         s_n = 4 * M
         data = O.fixed_keys(s_n, 64)
         what = "the first 4M x 64B keys of the stream"
@@ -1013,13 +1035,13 @@ def cpu_baseline(cfg, budget_s: float, gpu_out, P, torch):
     ok = None
     if gpu_out is not None:
         g = gpu_out.reshape(-1)[: dig.size].cpu().numpy().view(np.uint64)
-        if cfg == "cfg3" or cfg in ("cfg1", "cfg2", "cfg2r", "cfg4", "cfg5", "long", "place"):
+        if cfg == "cfg3" or cfg in ("cfg1", "cfg2", "cfg2r", "cfg4", "cfg5", "config4", "long", "place"):
             ok = bool((dig[: g.size] == g).all()) if g.size == dig.size else None
     res = {"value": round(s_n * reps / best / 1e9, 4), "unit": "Gkeys/s", "cores": thr, "kind": kind,
            "sample": f"{what}; {reps} passes per timing, best of 5 ({best:.2f} s wall, "
                      f"{best * thr:.1f} CPU-s)",
            "timer": "CLOCK_MONOTONIC_RAW", "host": cpus, "gpu_digests_equal_reference": ok}
-    if cfg in ("cfg2", "cfg2r", "cfg5"):
+    if cfg in ("cfg2", "cfg2r", "cfg5", "config4"):
         # BASELINE.md §3's other leg on the same box: one thread through
         # per-key pdht_hash over cfg1's 1M x 64 B keys
         k1 = O.fixed_keys(M, 64)

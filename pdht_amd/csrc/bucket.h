@@ -256,8 +256,11 @@ __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restr
   // the totals pass through LDS so that global loads and stores are
   // lane-contiguous (a thread's run of consecutive ranks would make every
   // wave instruction touch 64 lines)
+  // 64 KiB of totals + scratch: over the 64 KiB a workgroup may allocate on
+  // CDNA3, within gfx950's 160 KiB (the Makefile builds gfx950 only)
   __shared__ u64 tot[kBucketMaxRanks];
   __shared__ u64 scratch[kBaseThreads / 64];
+  static_assert(sizeof(tot) + sizeof(scratch) <= 160 * 1024, "gfx950 LDS per workgroup");
   if (tickets && threadIdx.x < 16) tickets[threadIdx.x] = 0;  // per-XCD tile tickets of the scatter kernels
   for (u32 r = threadIdx.x; r < nranks; r += kBaseThreads) tot[r] = totals[r];
   __syncthreads();

@@ -18,6 +18,14 @@ from dataclasses import dataclass
 MASK64 = (1 << 64) - 1
 
 
+def _grouped() -> bool:
+    """True inside an initialised process group -- of ANY size: at world size
+    1 the collectives still run (through RCCL when the group is "nccl"), so
+    a one-GPU run executes the same code path as an N-GPU one."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 @dataclass(frozen=True)
 class Shard:
     rank: int
@@ -70,7 +78,7 @@ def allreduce_fold(local_fold: int, device=None) -> int:
     import torch
     import torch.distributed as dist
     t = torch.tensor([_to_signed(local_fold)], dtype=torch.int64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _grouped():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item()) & MASK64
 
@@ -80,7 +88,7 @@ def allreduce_max(values, device=None) -> list[float]:
     import torch
     import torch.distributed as dist
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.tolist()]
 
@@ -90,7 +98,7 @@ def allreduce_min_int(v: int, device=None) -> int:
     import torch
     import torch.distributed as dist
     t = torch.tensor([int(v)], dtype=torch.int64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return int(t.item())
 
@@ -99,7 +107,7 @@ def allreduce_min_flag(ok: bool, device=None) -> bool:
     import torch
     import torch.distributed as dist
     t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(int(t.item()))
 
@@ -187,7 +195,7 @@ def per_rank_report(rank: int, local: int, world: int, n: int, bytes_per_key: fl
                 Gkeys_s=round(n / (kernel_ms / 1e3) / 1e9, 3),
                 frac=round(bytes_per_key * n / (kernel_ms / 1e3) / 1e9 / peak_GBps, 4),
                 wall_Gkeys_s=round(n * steps / elapsed_s / 1e9, 3))
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _grouped():
         allr = [None] * dist.get_world_size()
         dist.all_gather_object(allr, mine)
         backend = dist.get_backend()
@@ -200,5 +208,5 @@ def per_rank_report(rank: int, local: int, world: int, n: int, bytes_per_key: fl
 
 def barrier():
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _grouped():
         dist.barrier()

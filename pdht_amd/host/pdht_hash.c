@@ -20,6 +20,14 @@
 #include "pdht_city.h"
 #include "pdht_hip.h"
 
+/* The batch entry points write rank r of key i as a u32 at
+ * (char *)rank + i * sizeof(ptl_process_t): that needs the Portals 4 layout
+ * (8-byte union, .rank at offset 0), whichever header supplied the type.
+ * (C99: a negative array size fails the build.) */
+typedef char pdht_hip_ptl_process_is_8_bytes[sizeof(ptl_process_t) == 8 ? 1 : -1];
+typedef char pdht_hip_ptl_rank_at_offset_0[offsetof(ptl_process_t, rank) == 0 ? 1 : -1];
+typedef char pdht_hip_ptl_rank_is_u32[sizeof(((ptl_process_t *)0)->rank) == 4 ? 1 : -1];
+
 #ifndef PDHT_HIP_WITH_REAL_PDHT
 #define PDHT_SHIM_API __attribute__((visibility("default")))
 /* c->size stand-in; a real pdht build reads c->size instead. */

@@ -830,6 +830,39 @@ def test_cfg3_64M_mixed_full_fold(dev, folds, variant):
     assert f"{gpu_fold(d):016x}" == f["total"]
 
 
+@pytest.mark.parametrize("r", [1, 7])
+def test_cfg3_rank_shard(dev, folds, r):
+    """cfg3's weak shard of rank r at N > 1, hashed on this GPU exactly as
+    bench.py's rank r hashes it (lengths from key r*64M of the length stream,
+    bytes from word r << 40 of the key stream: bench.py cfg3 workload), against
+    the reference fold of that shard (gen_golden.py --multirank; the
+    reference places keys by contiguous slices, libpdht/hash.c:29)."""
+    f = folds["cfg3_city64_64M_mixed"]
+    n = f["n"]
+    want = f["ranks"][r]
+    lens = P.mixed_lengths(0x1E575EED1E575EED, r * n, n, 16, 256, device=dev)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    del lens
+    total = int(offs[-1].item())
+    assert total == want["total_bytes"]
+    words = P.splitmix64_fill(0x5EED5EED5EED5EED, r << 40, (total + 7) // 8, device=dev)
+    d = P.city64_var_batch(words.view(torch.uint8)[:total], offs)
+    assert f"{gpu_fold(d, r * n):016x}" == want["fold"]
+
+
+@pytest.mark.parametrize("r", [1, 7])
+def test_cfg4_rank_shard(dev, folds, r):
+    """cfg4's weak shard of rank r (keys [r*16M, (r+1)*16M) of the 64-B
+    stream), CityHashCrc128 on this GPU, against the reference fold of that
+    shard (128-bit digests fold from global entry 2*r*16M)."""
+    f = folds["cfg4_crc128_16M_x64"]
+    n = f["n"]
+    words = P.splitmix64_fill(0x5EED5EED5EED5EED, r * n * 8, n * 8, device=dev)
+    d = P.citycrc128_batch(words.view(torch.uint8).view(n, 64))
+    assert f"{gpu_fold(d, 2 * r * n):016x}" == f["rank_chunks"][r]
+
+
 def test_cfg5_all_shards_of_1B(dev, folds):
     """BASELINE configs[4] (1B x 64 B keys over 8 GPUs) on ONE GPU, one shard
     after another: shard j = keys [j*128M, (j+1)*128M), exactly the slice

@@ -273,3 +273,49 @@ def test_every_tuning_variant_is_documented():
     listed = {int(x) for x in re.findall(r"\b(\d+)\b", doc)}
     listed |= {n for lo, hi in re.findall(r"\b(\d+)-(\d+)\b", doc) for n in range(int(lo), int(hi) + 1)}
     assert used and not (used - listed), sorted(used - listed)
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "libpdht", "pdht_impl.h")),
+                    reason="reference sources absent (GPU box)")
+@pytest.mark.parametrize("flavour", ["libpdht", "libmpipdht"])
+def test_real_pdht_integration_branch_compiles(tmp_path, flavour):
+    """INTEGRATION.md §1's drop-in: pdht_amd/host/pdht_hash.c built with
+    -DPDHT_HIP_WITH_REAL_PDHT against the REAL pdht headers (libpdht/pdht_impl.h
+    -> pdht.h, or libmpipdht/pdht.h with -DPDHT_HIP_MPI_FLAVOUR), with the
+    reference's own flags (pdht.mk GCFLAGS: --std=c99 -O3
+    -D_POSIX_C_SOURCE=199309L).  The image lacks <portals4.h> and
+    <slurm/pmi.h>, so test-only stubs (tests/realpdht_stubs/) declare the
+    types pdht.h uses, ptl_process_t with the Portals 4 layout; the object's
+    static checks pin sizeof(ptl_process_t) == 8 with .rank a u32 at offset
+    0 -- the stride the batch entry points write.  Compile only: nothing of
+    the reference is linked or run."""
+    import subprocess
+    inc = [f"-I{REF}/libpdht"]
+    flags = []
+    if flavour == "libmpipdht":
+        mpi = [d for d in ("/opt/conda/include", "/usr/include/mpi", "/usr/lib/x86_64-linux-gnu/openmpi/include")
+               if os.path.exists(os.path.join(d, "mpi.h"))]
+        if not mpi:
+            pytest.skip("no mpi.h for libmpipdht/pdht.h")
+        inc = [f"-I{REF}/libmpipdht", f"-I{mpi[0]}"]
+        flags = ["-DPDHT_HIP_MPI_FLAVOUR"]
+    obj = str(tmp_path / "pdht_hash.o")
+    cmd = (["gcc", "--std=c99", "-O3", "-D_POSIX_C_SOURCE=199309L", "-fPIC", "-DPDHT_HIP_WITH_REAL_PDHT"] + flags
+           + ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "tests", "realpdht_stubs")] + inc
+           + ["-c", "-o", obj, os.path.join(ROOT, "pdht_amd", "host", "pdht_hash.c")])
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    # no diagnostics from OUR file (the reference's pdht_impl.h:68 redefines offsetof itself)
+    src = os.path.join(ROOT, "pdht_amd", "host", "pdht_hash.c")
+    ours = [ln for ln in p.stderr.splitlines() if ln.startswith(src + ":")]
+    assert not ours, p.stderr
+    syms = subprocess.run(["nm", obj], capture_output=True, text=True, check=True).stdout
+    defined = {ln.split()[-1] for ln in syms.splitlines() if " T " in ln}
+    assert {"pdht_hash", "pdht_sethash", "pdht_hash_batch", "pdht_hash_batch_dev"} <= defined
+    # the real build reads c->size, not the stand-in's rank count
+    assert "pdht_hip_shim_nranks" not in syms and "pdht_hip_table_init" not in syms
+    undef = {ln.split()[-1] for ln in syms.splitlines() if " U " in ln}
+    assert {"CityHash64", "pdht_place_batch_host", "pdht_place_batch_dev", "c"} <= undef, undef
