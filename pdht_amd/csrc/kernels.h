@@ -38,6 +38,54 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One LDS-DMA piece: 16 B per lane from global address g (per lane) to LDS
+// byte address lds + 16 * lane (lds wave-uniform), global_load_lds_dwordx4.
+// Issued from inline asm on purpose: the compiler's waitcnt pass cannot tell
+// an LDS-DMA target from the kernel's other LDS arrays, and after the
+// builtin form it puts s_waitcnt vmcnt(0) in front of EVERY later LDS access
+// (checked in the ISA) -- which would wait for the prefetch it is meant to
+// overlap.  The caller orders its reads of the slot with its own
+// s_waitcnt vmcnt(N) (loads, stores and LDS-DMA retire in issue order) and
+// must not overwrite a slot before its ds_reads are done (lgkmcnt(0)).
+// m0 carries the LDS base; it is saved and restored around the piece, and
+// one wait state separates the m0 write from the DMA (ISA hazard table).
+__device__ __forceinline__ void lds_dma16(const void *g, u32 lds) {
+  lds = __builtin_amdgcn_readfirstlane(lds);  // uniform by contract; into an SGPR for m0
+  u32 save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63] (the counter's range on
+// gfx950): all but the wave's n youngest vector-memory operations are done.
+__device__ __forceinline__ void vm_wait(u32 n) {
+#define PDHT_VMW(k) \
+  case k:           \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
+    break;
+  switch (__builtin_amdgcn_readfirstlane(n)) {
+    PDHT_VMW(1) PDHT_VMW(2) PDHT_VMW(3) PDHT_VMW(4) PDHT_VMW(5) PDHT_VMW(6) PDHT_VMW(7) PDHT_VMW(8)
+    PDHT_VMW(9) PDHT_VMW(10) PDHT_VMW(11) PDHT_VMW(12) PDHT_VMW(13) PDHT_VMW(14) PDHT_VMW(15) PDHT_VMW(16)
+    PDHT_VMW(17) PDHT_VMW(18) PDHT_VMW(19) PDHT_VMW(20) PDHT_VMW(21) PDHT_VMW(22) PDHT_VMW(23) PDHT_VMW(24)
+    PDHT_VMW(25) PDHT_VMW(26) PDHT_VMW(27) PDHT_VMW(28) PDHT_VMW(29) PDHT_VMW(30) PDHT_VMW(31) PDHT_VMW(32)
+    PDHT_VMW(33) PDHT_VMW(34) PDHT_VMW(35) PDHT_VMW(36) PDHT_VMW(37) PDHT_VMW(38) PDHT_VMW(39) PDHT_VMW(40)
+    PDHT_VMW(41) PDHT_VMW(42) PDHT_VMW(43) PDHT_VMW(44) PDHT_VMW(45) PDHT_VMW(46) PDHT_VMW(47) PDHT_VMW(48)
+    PDHT_VMW(49) PDHT_VMW(50) PDHT_VMW(51) PDHT_VMW(52) PDHT_VMW(53) PDHT_VMW(54) PDHT_VMW(55) PDHT_VMW(56)
+    PDHT_VMW(57) PDHT_VMW(58) PDHT_VMW(59) PDHT_VMW(60) PDHT_VMW(61) PDHT_VMW(62) PDHT_VMW(63)
+    default:
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      break;
+  }
+#undef PDHT_VMW
+}
+
 // --------------------------------------------------------------- readers ---
 // Key bytes in LDS at an arbitrary byte offset, r01-r03 form (tuning variant
 // 175 now): a span of N bytes is one run of N/4+1 dword reads from one base
