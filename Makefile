@@ -26,6 +26,7 @@ CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
 HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/runtime.h \
            pdht_amd/csrc/bucket.h pdht_amd/csrc/launch.h \
+           pdht_amd/csrc/tuning/kernels_tuning.h pdht_amd/csrc/tuning/launch_tuning.h \
            pdht_amd/csrc/pdht_hip_tuning.h include/pdht_hip.h include/pdht_city.h
 SHIM_HDR := include/pdht_hash.h include/pdht_hip.h include/pdht_city.h
 # the C-ABI in translation units that build in parallel (make -j)

@@ -797,19 +797,11 @@ struct TwoPass {
   u32 *iidx;            // [n] intermediate original indices
   u64 ntiles, nchunks;  // counting tiles; count-chunks of kTpChunkTiles tiles
   u64 SG, nsegf, nseg;  // count-chunks per segment; segments per f; segments
-  // pipelined passes (k_bucket_pass1_pf / _pass2_pf): where the lanes past a
-  // partial sub-tile store (every lane always stores, so a wave's count of
-  // outstanding vector-memory operations is exact), and every pass-2
-  // segment's {first intermediate row, rows} (k_bucket_segdesc)
-  uint8_t *trash;
-  u32 *segdesc;  // [nseg][2]
-  u32 *segrun;   // [nseg][C4]
   // keys of fine bucket f in the tiles before tile t (t <= ntiles)
   __device__ __forceinline__ u32 fine_before(u64 t, u32 f) const {
     return t < ntiles ? countsF[t * F + f] + chunksF[(t / kBucketChunk) * F + f] : (u32)totalsF[f];
   }
 };
-constexpr u32 kTrashBytes = 1u << 20;  // 2048 per-wave rows of 64 lanes x 8 B (a hot row would serialise in one L2 channel)
 
 // Two-pass counting.  One workgroup per count-chunk of kTpChunkTiles
 // counting tiles: the fine-bucket histogram of every tile -> countsF[t][f],
@@ -817,14 +809,11 @@ constexpr u32 kTrashBytes = 1u << 20;  // 2048 per-wave rows of 64 lanes x 8 B (
 // pass's per-tile rank rows are as large as the keys at high rank counts
 // (4096 tiles x 8192 ranks x 4 B = 128 MB for 16M keys, written, scanned and
 // read again); these are nranks/F and kTpChunkTiles times smaller.
-// PF (8-B keys: one 4096-key tile = 16 keys per thread): the next tile's
-// keys are loaded while this tile is hashed and counted.
-template <int L, bool PF = false>
+template <int L>
 __global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__restrict__ keys, u64 n, FastMod rk,
                                                             u32 nranks, u32 F, u32 *__restrict__ countsF,
                                                             u32 *__restrict__ chunkcnt, u64 ntiles) {
   constexpr int U = 128 / L;
-  static_assert(!PF || kBlock * U == kTpCountTile, "PF: one tile per iteration");
   extern __shared__ u32 hist[];  // [nranks]
   __shared__ u32 fh[kTpMaxDigits];
   const u32 fmask = F - 1;
@@ -832,45 +821,22 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__res
   for (u64 g = blockIdx.x; g < nchunks; g += gridDim.x) {
     for (u32 r = threadIdx.x; r < nranks; r += kBlock) hist[r] = 0;
     const u64 t1 = min((g + 1) * kTpChunkTiles, ntiles);
-    RegReader<L / 4> kn[PF ? U : 1];
-    if constexpr (PF) {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        load_key_regs<L, true>(keys, min(g * kTpChunkTiles * kTpCountTile + threadIdx.x + u * kBlock, n - 1), kn[u]);
-    }
     for (u64 t = g * kTpChunkTiles; t < t1; ++t) {
       if (threadIdx.x < F) fh[threadIdx.x] = 0;
       __syncthreads();
       const u64 k0 = t * kTpCountTile;
       const u64 kend = min(k0 + kTpCountTile, n);
-      if constexpr (PF) {
+      for (u64 i = k0 + threadIdx.x; i < kend; i += (u64)kBlock * U) {
         RegReader<L / 4> kr[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) kr[u] = kn[u];
-        if (t + 1 < t1)
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            load_key_regs<L, true>(keys, min(k0 + kTpCountTile + threadIdx.x + u * kBlock, n - 1), kn[u]);
+        for (int u = 0; u < U; ++u) load_key_regs<L, true>(keys, min(i + u * kBlock, n - 1), kr[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (k0 + threadIdx.x + u * kBlock < kend) {
+          if (i + u * kBlock < kend) {
             const u32 r = (u32)rk.mod(city64(kr[u], (u64)L));
             atomicAdd(&hist[r], 1u);
             atomicAdd(&fh[r & fmask], 1u);
           }
-      } else {
-        for (u64 i = k0 + threadIdx.x; i < kend; i += (u64)kBlock * U) {
-          RegReader<L / 4> kr[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) load_key_regs<L, true>(keys, min(i + u * kBlock, n - 1), kr[u]);
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (i + u * kBlock < kend) {
-              const u32 r = (u32)rk.mod(city64(kr[u], (u64)L));
-              atomicAdd(&hist[r], 1u);
-              atomicAdd(&fh[r & fmask], 1u);
-            }
-        }
       }
       __syncthreads();
       if (threadIdx.x < F) countsF[t * F + threadIdx.x] = fh[threadIdx.x];
@@ -906,39 +872,6 @@ __device__ __forceinline__ void digit_starts(const RunTab<false> &run, u32 ND, u
   }
 }
 
-// The same with the run table packed two u16 counters to a word (tile-local
-// positions < 2^16): thread k takes digits 2k and 2k+1, so each word has one
-// writer.
-template <int W, class Dst>
-__device__ __forceinline__ void digit_starts(const RunTab<true> &run, u32 ND, u32 *delta, u32 *tcount,
-                                             u32 *scan_scratch, const Dst &dst) {
-  const u32 d0 = 2 * threadIdx.x;
-  u32 s0 = 0, s1 = 0;
-  if (d0 < ND)
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      s0 += run.get(w, d0);
-      s1 += run.get(w, d0 + 1);
-    }
-  const u32 acc = block_exclusive_scan<W>(s0 + s1, scan_scratch);
-  if (d0 < ND) {
-    delta[d0] = dst(d0) - acc;
-    delta[d0 + 1] = dst(d0 + 1) - (acc + s0);
-    if (tcount) {
-      tcount[d0] = s0;
-      tcount[d0 + 1] = s1;
-    }
-    u32 a0 = acc, a1 = acc + s0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const u32 v0 = run.get(w, d0), v1 = run.get(w, d0 + 1);
-      run.t[(w * run.stride + d0) >> 1] = a0 | (a1 << 16);
-      a0 += v0;
-      a1 += v1;
-    }
-  }
-}
-
 // Pass-1 units are the counting tiles (kTpCountTile keys); both passes work
 // through their units in sub-tiles of W x KPL x 64 keys, carrying each
 // digit's next slot across sub-tiles.  Runs stay long with small sub-tiles
@@ -953,33 +886,25 @@ constexpr size_t pass1_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 2 + 1); 
 template <int W, int KPL>
 constexpr size_t pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
 
-// DBG (tuning build only, timing-only, wrong results): 1 = every sub-tile
-// stored contiguously at its own position, as if all runs were one.
-// PK: the run table packed (u16 counters, RunTab<true>): 4 KiB less LDS at 8
-// waves, so that 8 x 8 sub-tiles fit three workgroups per CU.
-template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0, bool DYN = false, bool PK = false>
+template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp, u32 *__restrict__ tickets) {
+void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   static_assert(kTpCountTile % kTile == 0, "sub-tiles of a counting tile");
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                            // [kTile] key pieces
   uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile] sub-tile-local index
   uint8_t *sdig = reinterpret_cast<uint8_t *>(sidx + kTile);     // [kTile] fine digit
-  __shared__ u32 runt[W * kTpMaxDigits / (PK ? 2 : 1)];
+  __shared__ u32 runt[W * kTpMaxDigits];
   __shared__ u32 running[kTpMaxDigits];  // next intermediate row of fine bucket f
   __shared__ u32 delta[kTpMaxDigits];
   __shared__ u32 tcount[kTpMaxDigits];
   __shared__ u32 scan_scratch[W];
-  const RunTab<PK> run{runt, tp.F};
+  const RunTab<false> run{runt, tp.F};
   const u32 fmask = tp.F - 1;
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u32 q0 = wave * kSub + lane;
-  __shared__ u32 s_ticket;
-  const XcdTickets tk(tickets, tp.ntiles);
-  TileOrder o(tp.ntiles);
-  if constexpr (DYN) o.t = tk.next(&s_ticket), o.end = tk.hi;
-  for (; o.t < o.end; o.t = DYN ? tk.next(&s_ticket) : o.t + o.step) {
+  for (TileOrder o(tp.ntiles); o.t < o.end; o.t += o.step) {
     const u64 t = o.t;
     const u64 tbase = t * kTpCountTile;
     const u32 ttn = (u32)min((u64)kTpCountTile, n - tbase);
@@ -988,7 +913,7 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass
     for (u32 s0 = 0; s0 < ttn; s0 += kTile) {
       const u32 tn = min(kTile, ttn - s0);
       const u64 sbase = tbase + s0;
-      for (u32 j = threadIdx.x; j < run.words(W); j += kB) runt[j] = 0;
+      for (u32 j = threadIdx.x; j < W * tp.F; j += kB) runt[j] = 0;
       RegReader<L / 4> kr[KPL];
 #pragma unroll
       for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(sbase + q0 + g * 64, n - 1), kr[g]);
@@ -1017,7 +942,7 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass
       for (int jj = 0; jj < KPL; ++jj) {
         const u32 j = jj * kB + threadIdx.x;
         if (j < tn) {
-          gp[jj] = (DBG ? (u32)sbase : delta[sdig[j]]) + j;
+          gp[jj] = delta[sdig[j]] + j;
           tp.iidx[gp[jj]] = (u32)(sbase + sidx[j]);
           *reinterpret_cast<u64 *>(tp.ikeys + (u64)gp[jj] * L) = stage[j];
         }
@@ -1042,9 +967,9 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass
   }
 }
 
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, int DBG = 0, bool DYN = false>
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict__ tickets) {
+void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   extern __shared__ u64 lds64[];
   u64 *stage = lds64;                                    // [kTile] digests, then key pieces
@@ -1060,11 +985,7 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict
   const u32 q0 = wave * kSub + lane;
   const u32 fbits = tp.fbits;
   auto coarse = [&](u64 h, u32) { return (u32)rk.mod(h) >> fbits; };
-  __shared__ u32 s_ticket;
-  const XcdTickets tk(tickets, tp.nseg);
-  TileOrder o(tp.nseg);
-  if constexpr (DYN) o.t = tk.next(&s_ticket), o.end = tk.hi;
-  for (; o.t < o.end; o.t = DYN ? tk.next(&s_ticket) : o.t + o.step) {
+  for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
     const u32 f = (u32)(o.t / tp.nsegf);
     const u64 g0 = (o.t % tp.nsegf) * tp.SG;
     const u64 g1 = min(g0 + tp.SG, tp.nchunks);
@@ -1114,365 +1035,11 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out, u32 *__restrict
           sidx[lp[g]] = ix[g];
         }
       __syncthreads();
-      if constexpr (DBG) {
-        __shared__ u32 dbase[1];
-        if (threadIdx.x == 0) dbase[0] = (u32)p0;
-        __syncthreads();
-        staged_store<L, KPL, kB>(stage, dbase, tn, kr, lp, q0, [](u64, u32) { return 0u; },
-                                 [&](u32 j) { return (u64)sidx[j]; }, out);
-      } else {
-        staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
-      }
+      staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
       __syncthreads();
       if (threadIdx.x < tp.C) running[threadIdx.x] += tcount[threadIdx.x];
     }
     __syncthreads();
-  }
-}
-
-// ------------------------------------------- pipelined two-pass bucketing ---
-// k_bucket_pass1 / _pass2 for 8-B keys with every sub-tile's input fetched
-// ONE SUB-TILE AHEAD by LDS-DMA into a per-wave slot (lds_dma16), under the
-// current sub-tile's hash / count / scan / rank / store phases.  In the
-// plain kernels each sub-tile starts with its own loads, and on gfx950 a
-// load wait is a vmcnt wait that also waits for every store issued before
-// it: each sub-tile paid the previous sub-tile's store acknowledgements plus
-// a load round trip (SQ_WAIT_ANY 52 % / 46 % of the wave cycles of pass 1 /
-// pass 2, profiles/r05/sq/).  Here the wait at the top of a sub-tile is
-// s_waitcnt vmcnt(#stores the wave issued in the previous sub-tile): the
-// DMA (and the row bases loaded beside it) done, the stores still in
-// flight.  That count must be exact, so a store instruction is issued or
-// skipped per WAVE (uniform branch), and the lanes of a wave's boundary
-// instruction past a partial sub-tile store into a per-wave trash row
-// (TwoPass::trash) instead of being masked off.  The slot costs LDS: the
-// staged shapes run fewer workgroups per CU than the plain ones.
-
-// Every pass-2 segment's {first intermediate row, rows} and its C bucket
-// bases (thread c of the segment: base[r] + keys of rank r = c*F + f in the
-// count-chunks before the segment), so that the pipelined pass 2 can DMA
-// them beside the segment's rows instead of loading them when it starts.
-// One thread per (segment, c < C4), C4 = C rounded up to 4 (16-B rows).
-__global__ __launch_bounds__(256) void k_bucket_segdesc(TwoPass tp, u32 nranks, u32 C4) {
-  const u64 e = (u64)blockIdx.x * 256 + threadIdx.x;
-  const u64 s = e / C4;
-  const u32 c = (u32)(e % C4);
-  if (s >= tp.nseg) return;
-  const u32 f = (u32)(s / tp.nsegf);
-  const u64 g0 = (s % tp.nsegf) * tp.SG;
-  if (c == 0) {
-    const u64 g1 = min(g0 + tp.SG, tp.nchunks);
-    const u32 lo = tp.fine_before(g0 * kTpChunkTiles, f);
-    const u32 hi = tp.fine_before(min(g1 * kTpChunkTiles, tp.ntiles), f);
-    tp.segdesc[2 * s] = (u32)tp.fbase[f] + lo;
-    tp.segdesc[2 * s + 1] = hi - lo;
-  }
-  const u32 r = c * tp.F + f;
-  tp.segrun[s * C4 + c] = c < tp.C && r < nranks ? (u32)tp.base[r] + tp.chunkcnt[g0 * nranks + r] : 0u;
-}
-
-// this wave's trash row (64 lanes x 8 B), one per wave of the grid
-__device__ __forceinline__ u64 *trash_row(const TwoPass &tp, u32 wave, u32 W) {
-  const u32 w = (blockIdx.x * W + wave) % (kTrashBytes / 512);
-  return reinterpret_cast<u64 *>(tp.trash) + 64 * w + (threadIdx.x & 63);
-}
-
-// A row of n32 u32 (16-B aligned, n32 a multiple of 4, <= 256) into LDS by
-// one wave's DMA piece.
-__device__ __forceinline__ void dma_row_u32(const u32 *row, u32 n32, void *lds) {
-  const u32 lane = threadIdx.x & 63;
-  if (lane * 4 < n32) lds_dma16(row + lane * 4, (u32)(uintptr_t)lds);
-}
-
-// LDS bytes of the pipelined passes (dynamic part)
-template <int W, int KPL>
-constexpr size_t pass1_pf_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 8 + 2 + 1); }
-template <int KPL>
-constexpr u32 pass2_pf_wave_slot() {  // a wave's key rows and index rows + 16-B alignment slack, whole KiB pieces
-  return ((KPL * 64 * 8 + 16 + 1023) / 1024 + (KPL * 64 * 4 + 16 + 1023) / 1024) * 1024;
-}
-template <int W, int KPL>
-constexpr size_t pass2_pf_lds_bytes() { return (size_t)W * pass2_pf_wave_slot<KPL>() + (size_t)W * KPL * 64 * (8 + 4); }
-
-// Reads of a constant-address-space pointer become scalar loads (lgkmcnt):
-// the pipelined kernels' uniform descriptor loads then stay out of vmcnt.
-typedef const __attribute__((address_space(4))) u32 cu32;
-__device__ __forceinline__ u32 sload(const u32 *p, u64 i) {
-  return reinterpret_cast<cu32 *>(reinterpret_cast<uintptr_t>(p))[i];
-}
-
-template <int W, int KPL, int WPE>
-__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass1_pf(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp) {
-  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
-  constexpr u32 kWaveBytes = kSub * 8;  // a wave's keys of a sub-tile
-  static_assert(W >= 2 && kTpCountTile % kTile == 0 && kWaveBytes % 1024 == 0,
-                "two base rows, whole sub-tiles, whole 1 KiB pieces");
-  constexpr u32 kSubs = kTpCountTile / kTile;
-  extern __shared__ u64 lds64[];
-  u64 *slot = lds64;                                             // [kTile] the next sub-tile's keys (DMA)
-  u64 *stage = slot + kTile;                                     // [kTile] keys in fine-bucket order
-  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile] sub-tile-local index
-  uint8_t *sdig = reinterpret_cast<uint8_t *>(sidx + kTile);     // [kTile] fine digit
-  __shared__ u32 runt[W * kTpMaxDigits];
-  __shared__ u32 running[kTpMaxDigits];  // next intermediate row of fine bucket f (thread f's own entry)
-  __shared__ u32 delta[kTpMaxDigits];
-  __shared__ u32 tcount[kTpMaxDigits];
-  __shared__ u32 scan_scratch[W];
-  __shared__ u32 fb[kTpMaxDigits];  // fbase (n < 2^32)
-  // a tile's countsF and chunksF rows (fine_before), by DMA, double-buffered by item parity
-  __shared__ __attribute__((aligned(16))) u32 tbr[2][2][kTpMaxDigits];
-  const RunTab<false> run{runt, tp.F};
-  const u32 fmask = tp.F - 1;
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const u32 q0 = wave * kSub + lane;
-  const u32 myslot = (u32)(uintptr_t)(slot + wave * kSub);
-  u64 *const trash = trash_row(tp, wave, W);
-  const TileOrder o(tp.ntiles);
-  if (o.t >= o.end) return;
-  auto full = [&](u64 t, u32 s) { return t * kTpCountTile + (u64)(s + 1) * kTile <= n; };
-  auto fetch = [&](u64 t, u32 s, u32 par) {
-    if (full(t, s)) {
-      const uint8_t *src = keys + (t * kTpCountTile + (u64)s * kTile + wave * kSub) * 8 + lane * 16;
-#pragma unroll
-      for (u32 j = 0; j < kWaveBytes / 1024; ++j) lds_dma16(src + j * 1024, myslot + j * 1024);
-    }
-    if (s == 0 && wave < 2)  // a new tile: its fine_before rows
-      dma_row_u32(wave == 0 ? tp.countsF + t * tp.F : tp.chunksF + (t / kBucketChunk) * tp.F, tp.F,
-                  tbr[par][wave]);
-  };
-  for (u32 f = threadIdx.x; f < tp.F; f += kB) fb[f] = (u32)tp.fbase[f];
-  u64 t = o.t;
-  u32 s = 0, it = 0;
-  fetch(t, 0, 0);
-  u32 nst = 0;  // store instructions this wave issued since its last DMA
-  while (true) {
-    const u32 par = it & 1;
-    const u64 tbase = t * kTpCountTile;
-    const u32 ttn = (u32)min((u64)kTpCountTile, n - tbase);
-    const u32 s0 = s * kTile;
-    const u32 tn = min(kTile, ttn - s0);
-    const u64 sbase = tbase + s0;
-    vm_wait(it == 0 ? 0u : nst);  // this item's DMA, issued before the last item's stores
-    __builtin_amdgcn_wave_barrier();
-    RegReader<2> kr[KPL];
-    if (full(t, s)) {
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) {
-        const u64 v = slot[wave * kSub + lane + 64 * g];
-        kr[g].d[0] = (u32)v;
-        kr[g].d[1] = (u32)(v >> 32);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is free for the next DMA
-    } else {  // the batch's last, partial sub-tile: plain (clamped) loads
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) load_key_regs<8, true>(keys, min(sbase + q0 + g * 64, n - 1), kr[g]);
-    }
-    // the next item of this workgroup: its keys (and rows) by DMA now
-    u64 t2 = t;
-    u32 s2 = s + 1;
-    if (s2 == kSubs || s0 + kTile >= ttn) {
-      t2 = t + o.step;
-      s2 = 0;
-    }
-    const bool more = t2 < o.end;
-    if (more) fetch(t2, s2, par ^ 1);
-    for (u32 j = threadIdx.x; j < W * tp.F; j += kB) runt[j] = 0;
-    u32 ff[KPL];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) ff[g] = (u32)rk.mod(city64(kr[g], (u64)8)) & fmask;
-    __syncthreads();  // (also: every wave's DMA of this item's rows has landed)
-    if (s == 0 && threadIdx.x < tp.F)  // this tile's row bases, thread f's own entry
-      running[threadIdx.x] = fb[threadIdx.x] + tbr[par][0][threadIdx.x] + tbr[par][1][threadIdx.x];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) run.add(wave, ff[g], 1u);
-    __syncthreads();
-    digit_starts<W>(run, tp.F, delta, tcount, scan_scratch, [&](u32 f) { return running[f]; });
-    __syncthreads();
-    u32 lp[KPL];
-    rank_groups<KPL>(run, wave, ff, q0, tn, tp.fbits, lp);
-#pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) {
-        stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
-        sidx[lp[g]] = (uint16_t)(q0 + g * 64);
-        sdig[lp[g]] = (uint8_t)ff[g];
-      }
-    __syncthreads();
-    nst = 0;
-#pragma unroll
-    for (int jj = 0; jj < KPL; ++jj) {
-      if (jj * kB + wave * 64 < tn) {  // wave-uniform: the instructions are issued or skipped per wave
-        const u32 j = jj * kB + threadIdx.x;
-        const bool ok = j < tn;
-        const u32 gp = delta[sdig[j]] + j;
-        u32 *pi = ok ? tp.iidx + gp : reinterpret_cast<u32 *>(trash);
-        u64 *pk = ok ? reinterpret_cast<u64 *>(tp.ikeys) + gp : trash;
-        *pi = (u32)(sbase + sidx[j]);
-        *pk = stage[j];
-        nst += 2;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < tp.F) running[threadIdx.x] += tcount[threadIdx.x];
-    if (!more) break;
-    t = t2;
-    s = s2;
-    ++it;
-  }
-}
-
-// Pass 2, pipelined: segments in the static XCD-contiguous order, each in
-// sub-tiles of kTile intermediate rows; a sub-tile's key rows and original
-// indices arrive by DMA (from the 16-B aligned address at or below its first
-// row: the slot carries 16 B of slack), and with a segment's first sub-tile
-// its bucket bases (k_bucket_segdesc), while the previous sub-tile is
-// processed.
-template <int W, int KPL, int WPE>
-__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass2_pf(FastMod rk, u32 nranks, TwoPass tp, OutSoA out, u64 n, u32 C4) {
-  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
-  constexpr u32 kWaveSlot = pass2_pf_wave_slot<KPL>();
-  constexpr u32 kKeyPieces = (kSub * 8 + 16 + 1023) / 1024, kIdxPieces = (kSub * 4 + 16 + 1023) / 1024;
-  extern __shared__ u64 lds64[];
-  uint8_t *slots = reinterpret_cast<uint8_t *>(lds64);          // [W][kWaveSlot]
-  u64 *stage = reinterpret_cast<u64 *>(slots + W * kWaveSlot);  // [kTile] digests, then key rows
-  u32 *sidx = reinterpret_cast<u32 *>(stage + kTile);          // [kTile] original index
-  __shared__ u32 runt[W * kTpMaxDigits];
-  __shared__ u32 running[kTpMaxDigits];  // next final slot of bucket c*F + f (thread c's own entry)
-  __shared__ u32 delta[kTpMaxDigits];
-  __shared__ u32 tcount[kTpMaxDigits];
-  __shared__ u32 scan_scratch[W];
-  __shared__ __attribute__((aligned(16))) u32 sbr[2][kTpMaxDigits];  // a segment's bucket bases, by parity
-  const RunTab<false> run{runt, tp.C};
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const u32 q0 = wave * kSub + lane;
-  const u64 *skeys = reinterpret_cast<const u64 *>(slots + wave * kWaveSlot);
-  const u32 *sidxs = reinterpret_cast<const u32 *>(slots + wave * kWaveSlot + kKeyPieces * 1024);
-  const u32 mykeys = (u32)(uintptr_t)skeys, myidx = (u32)(uintptr_t)sidxs;
-  u64 *const trash = trash_row(tp, wave, W);
-  const u32 fbits = tp.fbits;
-  auto coarse = [&](u64 h) { return (u32)rk.mod(h) >> fbits; };
-  const u64 kend = n * 8, iend = n * 4;  // DMA pieces never start past the arrays
-  auto fetch = [&](u64 sg, u64 p0, bool first_rows, u32 par) {
-    const u64 r0 = p0 + wave * kSub;
-    const u64 ka = ((r0 * 8) & ~(u64)15) + lane * 16, ia = ((r0 * 4) & ~(u64)15) + lane * 16;
-#pragma unroll
-    for (u32 j = 0; j < kKeyPieces; ++j)
-      if (ka + j * 1024 < kend) lds_dma16(tp.ikeys + ka + j * 1024, mykeys + j * 1024);
-#pragma unroll
-    for (u32 j = 0; j < kIdxPieces; ++j)
-      if (ia + j * 1024 < iend)
-        lds_dma16(reinterpret_cast<const uint8_t *>(tp.iidx) + ia + j * 1024, myidx + j * 1024);
-    if (first_rows && wave == 0) dma_row_u32(tp.segrun + sg * C4, C4, sbr[par]);
-  };
-  const TileOrder o(tp.nseg);
-  u64 seg = o.t;
-  u32 sst = 0, slen = 0;
-  for (; seg < o.end; seg += o.step) {  // the first non-empty segment
-    sst = sload(tp.segdesc, 2 * seg);
-    slen = sload(tp.segdesc, 2 * seg + 1);
-    if (slen) break;
-  }
-  if (seg >= o.end) return;
-  fetch(seg, sst, true, 0);
-  u32 k0 = 0, nst = 0, it = 0;
-  const u32 per_jj = 1 + (out.ptindex ? 1 : 0) + (out.index ? 1 : 0);
-  while (true) {
-    const u32 par = it & 1;
-    const u32 tn = min(kTile, slen - k0);
-    const u64 r0 = (u64)sst + k0 + wave * kSub;
-    const u32 ko = (u32)(r0 & 1), io = (u32)(r0 & 3);
-    vm_wait(it == 0 ? 0u : nst);  // this sub-tile's DMA, not the last sub-tile's stores
-    __builtin_amdgcn_wave_barrier();
-    RegReader<2> kr[KPL];
-    u32 ix[KPL];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) {
-      const u64 v = skeys[ko + lane + 64 * g];
-      kr[g].d[0] = (u32)v;
-      kr[g].d[1] = (u32)(v >> 32);
-      ix[g] = sidxs[io + lane + 64 * g];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is free for the next DMA
-    // the next sub-tile: this segment's next rows, or the next non-empty segment's first
-    u64 seg2 = seg;
-    u32 k02 = k0 + kTile, sst2 = sst, slen2 = slen;
-    if (k02 >= slen) {
-      k02 = 0;
-      for (seg2 = seg + o.step; seg2 < o.end; seg2 += o.step) {
-        sst2 = sload(tp.segdesc, 2 * seg2);
-        slen2 = sload(tp.segdesc, 2 * seg2 + 1);
-        if (slen2) break;
-      }
-    }
-    const bool more = seg2 < o.end;
-    if (more) fetch(seg2, (u64)sst2 + k02, k02 == 0, par ^ 1);
-    for (u32 j = threadIdx.x; j < W * tp.C; j += kB) runt[j] = 0;
-    u64 h[KPL];
-    u32 cc[KPL];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) {
-      h[g] = city64(kr[g], (u64)8);
-      cc[g] = coarse(h[g]);
-    }
-    __syncthreads();  // (also: wave 0's DMA of the segment's bases has landed)
-    if (k0 == 0 && threadIdx.x < tp.C) running[threadIdx.x] = sbr[par][threadIdx.x];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) run.add(wave, cc[g], 1u);
-    __syncthreads();
-    digit_starts<W>(run, tp.C, delta, tcount, scan_scratch, [&](u32 c) { return running[c]; });
-    __syncthreads();
-    u32 lp[KPL];
-    rank_groups<KPL>(run, wave, cc, q0, tn, tp.cbits, lp);
-#pragma unroll
-    for (int g = 0; g < KPL; ++g)
-      if (q0 + g * 64 < tn) {
-        stage[lp[g]] = h[g];
-        sidx[lp[g]] = ix[g];
-      }
-    __syncthreads();
-    // D: mbits, ptindex, index at the final slots (runs of consecutive lanes)
-    u32 gp[KPL];
-    nst = 0;
-#pragma unroll
-    for (int jj = 0; jj < KPL; ++jj) {
-      gp[jj] = 0;
-      if (jj * kB + wave * 64 < tn) {  // wave-uniform
-        const u32 j = jj * kB + threadIdx.x;
-        const bool ok = j < tn;
-        const u64 hv = stage[j];
-        gp[jj] = delta[coarse(hv)] + j;
-        *(ok ? out.mbits + gp[jj] : trash) = hv;
-        if (out.ptindex) *(ok ? out.ptindex + gp[jj] : reinterpret_cast<u32 *>(trash)) = (u32)out.pt.mod(hv);
-        if (out.index) *(ok ? out.index + gp[jj] : reinterpret_cast<u32 *>(trash)) = sidx[j];
-        nst += per_jj;
-      }
-    }
-    // E: the key rows through the same staging buffer
-    if (out.keys) {
-      __syncthreads();
-#pragma unroll
-      for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
-      __syncthreads();
-#pragma unroll
-      for (int jj = 0; jj < KPL; ++jj)
-        if (jj * kB + wave * 64 < tn) {
-          const u32 j = jj * kB + threadIdx.x;
-          *(j < tn ? reinterpret_cast<u64 *>(out.keys) + gp[jj] : trash) = stage[j];
-          nst += 1;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < tp.C) running[threadIdx.x] += tcount[threadIdx.x];
-    if (!more) break;
-    seg = seg2;
-    k0 = k02;
-    sst = sst2;
-    slen = slen2;
-    ++it;
   }
 }
 

@@ -38,83 +38,7 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One LDS-DMA piece: 16 B per lane from global address g (per lane) to LDS
-// byte address lds + 16 * lane (lds wave-uniform), global_load_lds_dwordx4.
-// Issued from inline asm on purpose: the compiler's waitcnt pass cannot tell
-// an LDS-DMA target from the kernel's other LDS arrays, and after the
-// builtin form it puts s_waitcnt vmcnt(0) in front of EVERY later LDS access
-// (checked in the ISA) -- which would wait for the prefetch it is meant to
-// overlap.  The caller orders its reads of the slot with its own
-// s_waitcnt vmcnt(N) (loads, stores and LDS-DMA retire in issue order) and
-// must not overwrite a slot before its ds_reads are done (lgkmcnt(0)).
-// m0 carries the LDS base; it is saved and restored around the piece, and
-// one wait state separates the m0 write from the DMA (ISA hazard table).
-__device__ __forceinline__ void lds_dma16(const void *g, u32 lds) {
-  lds = __builtin_amdgcn_readfirstlane(lds);  // uniform by contract; into an SGPR for m0
-  u32 save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(save)
-      : "v"(g), "s"(lds)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63] (the counter's range on
-// gfx950): all but the wave's n youngest vector-memory operations are done.
-__device__ __forceinline__ void vm_wait(u32 n) {
-#define PDHT_VMW(k) \
-  case k:           \
-    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
-    break;
-  switch (__builtin_amdgcn_readfirstlane(n)) {
-    PDHT_VMW(1) PDHT_VMW(2) PDHT_VMW(3) PDHT_VMW(4) PDHT_VMW(5) PDHT_VMW(6) PDHT_VMW(7) PDHT_VMW(8)
-    PDHT_VMW(9) PDHT_VMW(10) PDHT_VMW(11) PDHT_VMW(12) PDHT_VMW(13) PDHT_VMW(14) PDHT_VMW(15) PDHT_VMW(16)
-    PDHT_VMW(17) PDHT_VMW(18) PDHT_VMW(19) PDHT_VMW(20) PDHT_VMW(21) PDHT_VMW(22) PDHT_VMW(23) PDHT_VMW(24)
-    PDHT_VMW(25) PDHT_VMW(26) PDHT_VMW(27) PDHT_VMW(28) PDHT_VMW(29) PDHT_VMW(30) PDHT_VMW(31) PDHT_VMW(32)
-    PDHT_VMW(33) PDHT_VMW(34) PDHT_VMW(35) PDHT_VMW(36) PDHT_VMW(37) PDHT_VMW(38) PDHT_VMW(39) PDHT_VMW(40)
-    PDHT_VMW(41) PDHT_VMW(42) PDHT_VMW(43) PDHT_VMW(44) PDHT_VMW(45) PDHT_VMW(46) PDHT_VMW(47) PDHT_VMW(48)
-    PDHT_VMW(49) PDHT_VMW(50) PDHT_VMW(51) PDHT_VMW(52) PDHT_VMW(53) PDHT_VMW(54) PDHT_VMW(55) PDHT_VMW(56)
-    PDHT_VMW(57) PDHT_VMW(58) PDHT_VMW(59) PDHT_VMW(60) PDHT_VMW(61) PDHT_VMW(62) PDHT_VMW(63)
-    default:
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      break;
-  }
-#undef PDHT_VMW
-}
-
 // --------------------------------------------------------------- readers ---
-// Key bytes in LDS at an arbitrary byte offset, r01-r03 form (tuning variant
-// 175 now): a span of N bytes is one run of N/4+1 dword reads from one base
-// address (ds_read2_b32 with immediate offsets, a single wait) funnelled by
-// v_alignbyte_b32; the window carries 16 B of slack so the trailing dword
-// read stays in the array.
-struct LdsReaderFunnel {
-  const u32 *lds;
-  u32 base;
-  template <int N>
-  __device__ __forceinline__ Words<N / 4> span(u32 o) const {
-    const u32 a = base + o;
-    const u32 *p = lds + (a >> 2);
-    const u32 r = a & 3u;
-    u32 raw[N / 4 + 1];
-#pragma unroll
-    for (int j = 0; j <= N / 4; ++j) raw[j] = p[j];
-    Words<N / 4> w;
-#pragma unroll
-    for (int j = 0; j < N / 4; ++j) w.d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], r);
-    return w;
-  }
-  __device__ __forceinline__ u32 w32(u32 o) const { return span<4>(o).d[0]; }
-  __device__ __forceinline__ u32 b8(u32 o) const {
-    const u32 a = base + o;
-    return (lds[a >> 2] >> (8 * (a & 3u))) & 0xffu;
-  }
-};
-
 // Key bytes in LDS at an arbitrary byte offset (product, r04): spans as
 // UNALIGNED LDS loads.  gfx950 serves ds_read_b128 / ds_read_b64 /
 // ds_read_b32 at any byte address (HSA runs with unaligned access mode;
@@ -301,26 +225,12 @@ struct AlgoCrc128Seed {
 };
 
 // CRC-32C tables in LDS for batches that may hold keys > 900 B
-// (CityHashCrc256 path, city.c:407-517).  Two forms: the slicing-by-8 byte
-// tables (CrcLdsByteTab below, 8 KiB per workgroup, the product again from
-// r03) and the 6-bit-slice tables of city_core.h (Crc32c6Tables), 11 x 64
-// entries = 2816 B, every lookup conflict-free but 11 lookups per word (r02's
-// product; r01's byte tables lost to them on r01's long-key kernel, r03's
-// line-span kernel spends more on VALU than on bank conflicts).  r02's 5-bit
-// slices, 13 lookups per word, measured 2 % slower than 6-bit; from constant
-// memory the lookups are per-lane vector loads through the TA, 4x slower.
-struct CrcLds6Tab {
-  const u32 *t;  // [11][64]
-  __device__ __forceinline__ u32 crc64(u64 x) const {
-    const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    u32 r = t[0 * 64 + (lo & 63)] ^ t[1 * 64 + ((lo >> 6) & 63)] ^ t[2 * 64 + ((lo >> 12) & 63)] ^
-            t[3 * 64 + ((lo >> 18) & 63)] ^ t[4 * 64 + ((lo >> 24) & 63)];
-    r ^= t[5 * 64 + (__builtin_amdgcn_alignbit(hi, lo, 30) & 63)];
-    r ^= t[6 * 64 + ((hi >> 4) & 63)] ^ t[7 * 64 + ((hi >> 10) & 63)] ^ t[8 * 64 + ((hi >> 16) & 63)] ^
-         t[9 * 64 + ((hi >> 22) & 63)] ^ t[10 * 64 + (hi >> 28)];
-    return r;
-  }
-};
+// (CityHashCrc256 path, city.c:407-517): the slicing-by-8 byte tables below,
+// 8 KiB per workgroup.  r02's 6-bit-slice tables (city_core.h Crc32c6Tables,
+// 11 x 64 entries, conflict-free but 11 lookups per word; tuning/ variant
+// 150) and 5-bit slices measured slower on the r03 line-span kernel, which
+// spends more on VALU than on bank conflicts; from constant memory the
+// lookups are per-lane vector loads through the TA, 4x slower.
 // The product form (r03): plain slicing-by-8 byte tables (8 KiB, one copy),
 // each address one byte select: 8 lookups of ~2 VALU per word against the
 // 6-bit form's 11 of ~3.  Byte-indexed tables conflict in LDS (+72 % bank
@@ -335,37 +245,9 @@ struct CrcLdsByteTab {
            rd(4, hi & 255) ^ rd(5, (hi >> 8) & 255) ^ rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24);
   }
 };
-#ifdef PDHT_HIP_TUNING
-// Timing only: the CRC-32C of a word replaced by a fold (no table lookups):
-// what the lookups cost the long-key kernel (wrong digests).
-struct CrcNullTab {
-  const u32 *t;
-  __device__ __forceinline__ u32 crc64(u64 x) const { return (u32)x ^ (u32)(x >> 32) ^ t[0]; }
-};
-#endif
 
 template <int SB>
 struct CrcLdsSlices;
-template <>
-struct CrcLdsSlices<6> {
-  typedef CrcLds6Tab Tab;
-  static constexpr u32 kWords = 11 * 64;
-  __device__ static void fill(u32 *tab) {
-    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrc6Dev.t[k >> 6][k & 63];
-  }
-  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
-};
-#ifdef PDHT_HIP_TUNING
-template <>
-struct CrcLdsSlices<0> {  // CrcNullTab: the 6-bit form's launch shape, no lookups
-  typedef CrcNullTab Tab;
-  static constexpr u32 kWords = 64;
-  __device__ static void fill(u32 *tab) {
-    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = 0;
-  }
-  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
-};
-#endif
 template <>
 struct CrcLdsSlices<8> {  // CrcLdsByteTab: the product tables
   typedef CrcLdsByteTab Tab;
@@ -375,7 +257,7 @@ struct CrcLdsSlices<8> {  // CrcLdsByteTab: the product tables
   }
   __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
 };
-constexpr int kCrcSlices = 8;  // the product's CRC-32C tables (tuning variant 150: 6)
+constexpr int kCrcSlices = 8;  // the product's CRC-32C tables
 template <class Base, int SB = kCrcSlices>
 struct CrcLds : Base {
   static constexpr bool kCrcLds = true;
@@ -447,27 +329,6 @@ struct AlgoFoldVar {
   }
 };
 
-#ifdef PDHT_HIP_TUNING
-// Tuning-only calibrations of the variable-length window kernel: the digest
-// is the key length (no key byte is read from LDS), so the kernel is its
-// window DMA, offsets loads and digest stores alone.
-struct AlgoLenOnly {
-  typedef u64 Out;
-  template <class R>
-  __device__ __forceinline__ Out operator()(const R &, u64 len) const {
-    return len;
-  }
-};
-// Timing only: CityHash64 twice per key (the second over the key minus its
-// first byte), to see what the hash arithmetic itself costs a kernel.
-struct AlgoCity64x2 {
-  typedef u64 Out;
-  template <class R>
-  __device__ __forceinline__ Out operator()(const R &r, u64 len) const {
-    return city64(r, len) ^ (len ? city64(Shifted<R>{r, 1u}, len - 1) : 0);
-  }
-};
-#endif
 
 // ----------------------------------------------------------------- sinks ---
 // Where a digest goes.  init()/flush() run once per workgroup around the
@@ -507,71 +368,8 @@ struct Sink128T {
 };
 typedef Sink64T<false> Sink64;
 
-// 64-bit digests stored 16 B per lane: every even lane takes its odd
-// neighbour's digest (two DPP row_shl:1 moves) and stores both with one
-// dwordx4, so a wave's 512 B of digests leave as 32 lane-stores instead of
-// 64 (i must be 64-aligned tile base + lane, as in every kernel here; a lane
-// whose partner is inactive -- past the batch's end, or in another branch of
-// a divergent hash -- stores its own digest alone).
-template <bool NTS = true>
-struct Sink64x2T {
-  static constexpr u32 kHist = 1;
-  u32 *lds_hist;
-  u64 *out;
-  __device__ __forceinline__ void init() {}
-  __device__ __forceinline__ void put(u64 i, u64 h) {
-    const u32 lo = (u32)h, hi = (u32)(h >> 32);
-    const u32 lo1 = __builtin_amdgcn_mov_dpp(lo, 0x101, 0xf, 0xf, false);  // row_shl:1: lane l <- l+1
-    const u32 hi1 = __builtin_amdgcn_mov_dpp(hi, 0x101, 0xf, 0xf, false);
-    const u32 lane = (u32)i & 63;
-    // partner = the other lane of the pair; the two may sit in different
-    // divergent branches (then each stores its own digest)
-    const bool partner = (__builtin_amdgcn_read_exec() >> (lane ^ 1)) & 1;
-    if ((lane & 1) == 0 && partner)
-      st<NTS>(u32x4{lo, hi, lo1, hi1}, reinterpret_cast<u32x4 *>(out + i));
-    else if (!partner)
-      st<NTS>(h, out + i);
-  }
-  __device__ __forceinline__ void flush() {}
-  __host__ Sink64x2T shift(u64 k0) const { return Sink64x2T{lds_hist, out + k0}; }
-};
 typedef Sink128T<false> Sink128;
 
-#ifdef PDHT_HIP_TUNING
-// Calibration only: digests dropped (a kernel's loads alone).
-struct SinkNone {
-  static constexpr u32 kHist = 1;
-  u32 *lds_hist;
-  u64 *out;
-  __device__ __forceinline__ void init() {}
-  __device__ __forceinline__ void put(u64, u64 h) {
-    if (h == 0x0123456789abcdefull) out[0] = h;  // keeps the digest live, never taken
-  }
-  __device__ __forceinline__ void flush() {}
-};
-// Calibration only: every digest stored, but into the first 32 KiB of out
-// (L2-resident): the store instructions without their HBM writes.
-struct SinkSmall {
-  static constexpr u32 kHist = 1;
-  u32 *lds_hist;
-  u64 *out;
-  __device__ __forceinline__ void init() {}
-  __device__ __forceinline__ void put(u64 i, u64 h) { out[i & 4095] = h; }
-  __device__ __forceinline__ void flush() {}
-};
-// Calibration only: nt digest stores wrapped into the first 2^BITS digests
-// of out (2^BITS x 8 B: L2-sized to Infinity-Cache-sized destinations).
-template <int BITS>
-struct SinkRing {
-  static constexpr u32 kHist = 1;
-  u32 *lds_hist;
-  u64 *out;
-  __device__ __forceinline__ void init() {}
-  __device__ __forceinline__ void put(u64 i, u64 h) { st<true>(h, out + (i & ((1ull << BITS) - 1))); }
-  __device__ __forceinline__ void flush() {}
-  __host__ SinkRing shift(u64) const { return *this; }
-};
-#endif
 
 // The same sink with non-temporal stores (identity for other sinks).
 template <class S>
@@ -886,128 +684,6 @@ __global__ __launch_bounds__(kBlock) void k_window(const uint8_t *__restrict__ b
     __builtin_amdgcn_wave_barrier();  // window reused by the next tile
   }
   sink.flush();
-}
-
-// ------------------------------------------------ pipelined window kernel ---
-// Offset-indexed keys with 64-bit digests, one LDS window per wave as in
-// k_window, but with every memory latency except the window DMA's taken off a
-// tile's critical path.  k_window's tile is a chain of four dependent memory
-// round trips -- offsets (a vmcnt(0) wait that also waits for the previous
-// tile's digest store to be acknowledged), two scalar loads of the window
-// bounds, then the DMA.  Here:
-//   * the offsets of the wave's next tile are loaded while this tile's window
-//     streams in: one dwordx4 per lane = offsets[i], offsets[i+1] (index
-//     clamped to n-1, so the load is always issued and the clamped lanes read
-//     offsets[n]); the window is [lane 0's start, lane 63's end) by readlane --
-//     no scalar loads, whose lgkmcnt wait would meet the LDS reads;
-//   * a tile's digests are stored one tile late, right after the next tile's
-//     DMA and offsets load are issued, as a raw buffer store whose range
-//     check drops the lanes past n (always issued, even with no valid lane);
-//   * so the wait for a window is s_waitcnt vmcnt(2): on gfx950 loads, stores
-//     and LDS-DMA count together in issue order (MI355X_MICROARCH.md,
-//     "s_waitcnt vmcnt(N)"), and the two youngest operations are exactly that
-//     offsets load and that store -- the wait never includes a store.
-// G = tiles a wave takes in a row before jumping by the grid (1: the grid
-// stride of k_window; 16: r02's grouped order, consecutive windows per wave).
-// RING (calibration only): digests of tile t go to out + 64 * (t % RING), an
-// L2-resident destination -- the kernel without its HBM writes.
-// SAUX: cache-policy bits of the digest stores (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
-template <int WIN, int G, class Algo, int AUX = 2, class LR = LdsReader, u64 RING = 0, int SAUX = AUX>
-__global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restrict__ bytes,
-                                                        const u64 *__restrict__ offsets, u64 obase, u64 n,
-                                                        Algo algo, u64 *__restrict__ out) {
-  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
-  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
-  algo_init(algo);
-  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u32 lane = threadIdx.x & 63;
-  const u64 ntiles = (n + 63) >> 6;
-  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
-  u32 *lds = win_all + wave * (WIN / 4);
-  const u64 base = (u64)(uintptr_t)bytes;
-  // tile order: runs of G consecutive tiles, run r of wave w = gw + r * nwaves
-  const u64 gw = (u64)blockIdx.x * kWavesPerBlock + wave;
-  auto next = [&](u64 t) -> u64 {
-    if (G > 1 && (t + 1) % G != 0) return t + 1;
-    return (t / G + nwaves) * G;
-  };
-  u64 t = gw * G;
-  if (t >= ntiles) return;
-  // key i's bounds: offsets[min(i, n-1)] and the next entry (n >= 1 here)
-  auto bounds = [&](u64 tt, u64 &a, u64 &e) {
-    const u64 *p = offsets + ((tt << 6) + lane < n ? (tt << 6) + lane : n - 1);
-    a = p[0];
-    e = p[1];
-  };
-  auto rd64 = [](u64 v, u32 l) -> u64 {
-    return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) |
-           ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
-  };
-  u64 a, e;
-  bounds(t, a, e);
-  u64 hprev = 0, tprev = ~0ull;  // digest of the previous tile (none yet)
-  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
-  while (true) {
-    const u64 k0 = t << 6;
-    const u64 i = k0 + lane;
-    const bool valid = i < n;
-    const u64 start = a - obase;
-    const u64 end = e - obase;
-    const u64 first = rd64(a, 0) - obase;
-    const u64 whi = rd64(e, 63) - obase;
-    const u64 wlo = (base + first) & ~(u64)15;  // absolute, as in k_window
-    const u64 span = whi > first ? base + whi - wlo : 0;
-    const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
-    const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)wlo);
-#pragma unroll
-    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
-      if ((u32)j * 1024 < wbytes) {  // wave-uniform
-        if ((u32)j * 1024 + lane * 16 < wbytes)
-          __builtin_amdgcn_global_load_lds(
-              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
-              (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, AUX);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // the next tile's offsets (always issued: clamped index; past the end the
-    // loop stops before they are used)
-    const u64 tn = next(t);
-    u64 an, en;
-    bounds(tn, an, en);
-    __builtin_amdgcn_sched_barrier(0);
-    // the previous tile's digests (always issued; records past n dropped)
-    {
-      const u64 pk = tprev << 6;
-      const u32 nrec = tprev == ~0ull ? 0u : (u32)((n - pk < 64 ? n - pk : 64) * 8);
-      const u64 dst = tprev == ~0ull ? 0 : RING ? (tprev % RING) << 6 : pk;
-      __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + dst, 0, nrec, 0x00020000);
-      const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
-      __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    if (valid) {
-      const u64 len = end - start;
-      if (base + end - wlo <= wbytes)
-        hprev = algo(LR{lds, (u32)(base + start - wlo)}, len);
-      else
-        hprev = algo(GlobalReader{bytes + start}, len);
-    }
-    tprev = t;
-    __builtin_amdgcn_wave_barrier();  // window reused by the next tile
-    if (tn >= ntiles) break;
-    t = tn;
-    a = an;
-    e = en;
-  }
-  // the last tile's digests
-  const u64 pk = tprev << 6;
-  const u32 nrec = (u32)((n - pk < 64 ? n - pk : 64) * 8);
-  __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(out + (RING ? (tprev % RING) << 6 : pk), 0, nrec, 0x00020000);
-  const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
 }
 
 // ---------------------------------------------------------- long keys ---

@@ -7,6 +7,11 @@
 namespace pdht {
 
 constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wave (12 KiB)
+}  // namespace pdht
+#ifdef PDHT_HIP_TUNING
+#include "tuning/launch_tuning.h"  // the A/B harness's alternative shapes: one hook per path below
+#endif
+namespace pdht {
 // Kernel tags (pdht_hip_last_kernel): the kernel and its launch shape, so a
 // profile taken of one shape (profiles/traffic_*.json) is never attributed to
 // another.
@@ -29,6 +34,9 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
                          hipStream_t st, int dev, u64 blocks) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt snt = NtSink<Sink>::make(sink);
+#ifdef PDHT_HIP_TUNING
+  if (tuning_small(keylen, k, n, algo, sink, st, dev, blocks) != kNoVariant) return;
+#endif
   if constexpr (std::is_same<Sink, SinkPlace>::value) {
     // With a histogram: 1024-thread workgroups, 2 per CU.  Every workgroup
     // flushes its LDS bins with one device-scope atomic per bin, and those
@@ -39,21 +47,6 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // (r02, tools/abbench.py place8_*: 8-B keys stream best at ONE such
     // workgroup per CU -- 0.80 of the roofline against 0.74 at two, half the
     // flushes again; 16-B keys stay at two)
-#ifdef PDHT_HIP_TUNING
-    if (sink.hist && keylen == 8 && (tuning_variant() == 219 || tuning_variant() == 220)) {
-      // r04: 4 (the shape before) / 16 keys per lane in flight
-      if (tuning_variant() == 219) {
-        g_kernel = "k_fixed_direct<8,4,nt,1024>@1";
-        k_fixed_direct<8, 4, Algo, SinkNt, true, 1024>
-            <<<grid_for((blocks + 15) / 16, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
-      } else {
-        g_kernel = "k_fixed_direct<8,16,nt,1024>@1";
-        k_fixed_direct<8, 16, Algo, SinkNt, true, 1024>
-            <<<grid_for((blocks + 63) / 64, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
-      }
-      return;
-    }
-#endif
     // 8 keys per lane in flight (late r04, HBM-resident keys: 0.621 -> 0.681
     // against 4; 16: 0.629; profiles/r04/ab/ab_placerot_shapes.log)
     if (sink.hist && keylen == 8) {
@@ -62,14 +55,6 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
           <<<grid_for((blocks + 31) / 32, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
       return;
     }
-#ifdef PDHT_HIP_TUNING
-    if (sink.hist && keylen == 16 && tuning_variant() == 225) {  // r04: 4 keys per lane in flight
-      g_kernel = "k_fixed_direct<16,4,nt,1024>@2";
-      k_fixed_direct<16, 4, Algo, SinkNt, true, 1024>
-          <<<grid_for((blocks + 15) / 16, 2, dev), 1024, 0, st>>>(k, n, algo, snt);
-      return;
-    }
-#endif
     if (sink.hist && keylen == 16) {
       g_kernel = "k_fixed_direct<16,2,nt,1024>@2";
       k_fixed_direct<16, 2, Algo, SinkNt, true, 1024>
@@ -77,25 +62,6 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
       return;
     }
   }
-#ifdef PDHT_HIP_TUNING
-  if (keylen == 8 && tuning_variant() >= 221 && tuning_variant() <= 223) {
-    // r04: plain loads (221, the shape before), 8 keys per lane (222; 223 as 1024-thread @1)
-    if (tuning_variant() == 221) {
-      g_kernel = "k_fixed_direct<8,4,nt-store>@8";
-      k_fixed_direct<8, 4, Algo, SinkNt, false><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo,
-                                                                                                      snt);
-    } else if (tuning_variant() == 222) {
-      g_kernel = "k_fixed_direct<8,8,nt>@8";
-      k_fixed_direct<8, 8, Algo, SinkNt, true><<<grid_for((blocks + 7) / 8, 8, dev), kBlock, 0, st>>>(k, n, algo,
-                                                                                                     snt);
-    } else {
-      g_kernel = "k_fixed_direct<8,8,nt,1024>@1";
-      k_fixed_direct<8, 8, Algo, SinkNt, true, 1024>
-          <<<grid_for((blocks + 31) / 32, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
-    }
-    return;
-  }
-#endif
   if (keylen == 8) {
     // non-temporal loads since late r04: 0.659 -> 0.712 with HBM-resident
     // keys (r01's plain loads were chosen on a cache-resident buffer;
@@ -104,26 +70,10 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     k_fixed_direct<8, 4, Algo, SinkNt, true><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(
         k, n, algo, snt);
   } else if (keylen == 16) {
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 226) {  // r04: 4 keys per lane in flight
-      g_kernel = "k_fixed_direct<16,4,nt>@8";
-      k_fixed_direct<16, 4, Algo, SinkNt, true><<<grid_for((blocks + 3) / 4, 8, dev), kBlock, 0, st>>>(k, n, algo,
-                                                                                                      snt);
-      return;
-    }
-#endif
     g_kernel = "k_fixed_direct<16,2,nt>@8";
     k_fixed_direct<16, 2, Algo, SinkNt, true><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(
         k, n, algo, snt);
   } else {
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 224) {  // plain loads and stores for 32-B keys (the shape before late r04)
-      g_kernel = "k_fixed_direct<32,2>@8";
-      k_fixed_direct<32, 2, Algo, Sink><<<grid_for((blocks + 1) / 2, 8, dev), kBlock, 0, st>>>(k, n, algo,
-                                                                                              sink);
-      return;
-    }
-#endif
     // non-temporal loads and stores since late r04: 0.628 -> 0.688 with
     // HBM-resident keys (profiles/r04/ab/ab_city32rot.log)
     g_kernel = "k_fixed_direct<32,2,nt>@8";
@@ -156,14 +106,7 @@ static bool sink_has_hist(const Sink &s) {
 constexpr u64 kLaunchBytes = 512ull << 20;
 static u64 launch_chunk_bytes() {
 #ifdef PDHT_HIP_TUNING
-  switch (tuning_variant()) {  // 114-118: chunk 256 MiB / 1 GiB / 2 GiB / 4 GiB / one launch
-    case 114: return 256ull << 20;
-    case 115: return 1ull << 30;
-    case 116: return 2ull << 30;
-    case 117: return 4ull << 30;
-    case 118: return ~0ull;
-    default: break;
-  }
+  if (const u64 b = tuning_chunk_bytes()) return b;
 #endif
   return kLaunchBytes;
 }
@@ -215,53 +158,8 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
   constexpr bool kShort = !HasCrcLds<Algo>::value;
   if (kShort && packed && keylen == 64 && al16) {
 #ifdef PDHT_HIP_TUNING
-    if constexpr (kShort) {
-      if (tuning_variant() == 7) {  // one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
-        g_kernel = "k_fixed_xpose64<nt,d1>@4";
-        k_fixed_xpose64<Algo, SinkNt, true, 1><<<grid_for((n + 255) / 256, 4, dev), kBlock, 0, st>>>(
-            k, n, algo, sink_nt);
-        HIP_TRY(hipGetLastError());
-        return 0;
-      }
-      if (tuning_variant() == 80 || tuning_variant() == 81) {  // 1024-thread workgroups, 1 / 2 per CU
-        g_kernel = tuning_variant() == 80 ? "k_fixed_xpose64<nt,d2,1024>@1" : "k_fixed_xpose64<nt,d2,1024>@2";
-        k_fixed_xpose64<Algo, SinkNt, true, 2, 1024>
-            <<<grid_for((n + 1023) / 1024, tuning_variant() == 80 ? 1 : 2, dev), 1024, 0, st>>>(k, n, algo,
-                                                                                                sink_nt);
-        HIP_TRY(hipGetLastError());
-        return 0;
-      }
-      if (tuning_variant() == 82) {  // the 256-thread shape whatever the histogram
-        g_kernel = "k_fixed_xpose64<nt,d2>@3";
-        k_fixed_xpose64<Algo, SinkNt, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
-            k, n, algo, sink_nt);
-        HIP_TRY(hipGetLastError());
-        return 0;
-      }
-      if (tuning_variant() == 206) {  // s_setprio 1 around each wave's prefetch issue
-        g_kernel = "k_fixed_xpose64<nt,d2,prio1>@3";
-        k_fixed_xpose64<Algo, SinkNt, true, 2, kBlock, 1><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
-            k, n, algo, sink_nt);
-        HIP_TRY(hipGetLastError());
-        return 0;
-      }
-      if constexpr (std::is_same<Sink, Sink64>::value) {
-        if (tuning_variant() == 188) {  // digests stored 16 B per lane (even lanes, DPP pairs)
-          g_kernel = "k_fixed_xpose64<nt,d2,st16>@3";
-          k_fixed_xpose64<Algo, Sink64x2T<true>, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
-              k, n, algo, Sink64x2T<true>{nullptr, sink.out});
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
-      }
-      if (tuning_variant() == 26) {  // plain digest stores (r01: 2-6 % slower)
-        g_kernel = "k_fixed_xpose64<nt-load,plain-store,d2>@3";
-        k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(
-            k, n, algo, sink);
-        HIP_TRY(hipGetLastError());
-        return 0;
-      }
-    }
+    if constexpr (kShort)
+      if (int rc = tuning_xpose64(k, n, algo, sink, st, dev); rc != kNoVariant) return rc;
 #endif
     // measured fastest (profiles/r01/kbench_*): non-temporal loads
     // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU.
@@ -292,15 +190,8 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
     // (VGPR-bound to 3 waves per SIMD)
     const unsigned g = grid_for(blocks, 8, dev);
 #ifdef PDHT_HIP_TUNING
-    if (al16 && stride % 16 == 0 && (tuning_variant() == 190 || tuning_variant() == 191)) {
-      // CityHashCrc256Long's block loop as a 128-B line stream (kLongStream)
-      const int pc = tuning_variant() == 190 ? 8 : 4;
-      g_kernel = pc == 8 ? "k_global<fixed,a16,stream>@8" : "k_global<fixed,a16,stream>@4";
-      k_global<false, Algo, SinkNt, true, kLongStream><<<grid_for(blocks, pc, dev), kBlock, 0, st>>>(
-          k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
+    if (al16 && stride % 16 == 0)
+      if (int rc = tuning_crc_long(k, stride, keylen, n, algo, sink, st, dev, blocks); rc != kNoVariant) return rc;
 #endif
     if (al16 && stride % 16 == 0) {
       g_kernel = "k_global<fixed,a16,lines>@8";
@@ -324,13 +215,8 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
       constexpr int kPerCu = 2;
       if (al16 && stride % 16 == 0) {
 #ifdef PDHT_HIP_TUNING
-        if (tuning_variant() == 96) {  // r02 before the line spans: 240-B / 64-B spans as the algorithm reads them
-          g_kernel = "k_global<fixed,a16>@2";
-          k_global<false, Algo, SinkNt, true><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
-              k, nullptr, 0, stride, keylen, n, algo, sink_nt);
-          HIP_TRY(hipGetLastError());
-          return 0;
-        }
+        if (int rc = tuning_long_walk(k, stride, keylen, n, algo, sink, st, dev, blocks, kPerCu); rc != kNoVariant)
+          return rc;
 #endif
         g_kernel = "k_global<fixed,a16,lines>@2";
         k_global<false, Algo, SinkNt, true, kLongLines><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
@@ -400,79 +286,7 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
   const u64 wb = ((n + 63) / 64 + 3) / 4;  // blocks of 4 wave-tiles
   bool wide = nbytes / n > 160;
 #ifdef PDHT_HIP_TUNING
-  if (tuning_variant() == 12) wide = false;
-  if (tuning_variant() == 13) wide = true;
-  if constexpr (std::is_same<Algo, AlgoCity64>::value && std::is_same<Sink, Sink64>::value) {
-    const int v = tuning_variant();
-    if (v >= 180 && v <= 187) {  // cache policies of the pipe kernel's DMA / digest stores
-      auto go = [&](auto kern, const char *tag) {
-        g_kernel = tag;
-        kern<<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo, sink.out);
-      };
-      switch (v) {
-        case 180: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 0>, "k_window_pipe<dma nt,st plain>"); break;
-        case 181: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 1>, "k_window_pipe<dma nt,st sc0>"); break;
-        case 182: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 16>, "k_window_pipe<dma nt,st sc1>"); break;
-        case 183: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 18>, "k_window_pipe<dma nt,st sc1 nt>"); break;
-        case 184: go(k_window_pipe<10224, 1, Algo, 2, LdsReader, 0, 19>, "k_window_pipe<dma nt,st sc0 sc1 nt>"); break;
-        case 185: go(k_window_pipe<10224, 1, Algo, 0, LdsReader, 0, 2>, "k_window_pipe<dma plain,st nt>"); break;
-        case 186: go(k_window_pipe<10224, 1, Algo, 3, LdsReader, 0, 2>, "k_window_pipe<dma sc0 nt,st nt>"); break;
-        default: go(k_window_pipe<10224, 1, Algo, 16, LdsReader, 0, 2>, "k_window_pipe<dma sc1,st nt>"); break;
-      }
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-    if (v == 203 || v == 204) {  // the product window kernel, s_setprio around the fetch phase
-      g_kernel = v == 203 ? "k_window<var,nt,10224,prio3>@4" : "k_window<var,nt,10224,prio1>@4";
-      if (v == 203)
-        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReader, 3><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
-      else
-        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReader, 1><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-            b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-    if (v == 189) {  // the product window kernel, digests stored 16 B per lane
-      g_kernel = "k_window<var,nt,10224,st16>@4";
-      k_window<10224, true, Algo, Sink64x2T<true>, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-          b, offsets, obase, 0, 0, n, algo, Sink64x2T<true>{nullptr, sink.out});
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-    if (v == 174 || v == 175) {  // 174: pipe kernel, r03 funnel reader; 175: product kernel, r03 reader
-      if (v == 174) {
-        g_kernel = "k_window_pipe<var,10224,G1,funnel>@4";
-        k_window_pipe<10224, 1, Algo, 2, LdsReaderFunnel><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
-            b, offsets, obase, n, algo, sink.out);
-      } else {
-        g_kernel = "k_window<var,nt,10224,funnel>@4";
-        k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReaderFunnel>
-            <<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n, algo,
-                                                     Sink64T<true>{nullptr, sink.out});
-      }
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-    if (v >= 170 && v <= 173) {  // pipelined window kernel (offsets a tile ahead, stores a tile late)
-      const int pc = v == 173 ? 3 : 4;
-      if (v == 170 || v == 173) {
-        g_kernel = v == 170 ? "k_window_pipe<var,10224,G1>@4" : "k_window_pipe<var,10224,G1>@3";
-        k_window_pipe<10224, 1, Algo, 2><<<grid_for(wb, pc, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                     sink.out);
-      } else if (v == 171) {
-        g_kernel = "k_window_pipe<var,10224,G4>@4";
-        k_window_pipe<10224, 4, Algo, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                    sink.out);
-      } else {
-        g_kernel = "k_window_pipe<var,10224,G16>@4";
-        k_window_pipe<10224, 16, Algo, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n, algo,
-                                                                                     sink.out);
-      }
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-  }
+  if (int rc = tuning_var(b, offsets, obase, n, algo, sink, st, dev, wb, wide); rc != kNoVariant) return rc;
 #endif
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";
@@ -483,14 +297,6 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
     // window DMA (r04, interleaved: cfg3 +1.8 %, cfg3c +0.8 %; 3 equal to 1;
     // tuning 205 = without)
     g_kernel = "k_window<var,nt,10224>@4";
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 205) {
-      k_window<10224, true, Algo, SinkNt, 2><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0,
-                                                                                      n, algo, sink_nt);
-      HIP_TRY(hipGetLastError());
-      return 0;
-    }
-#endif
     k_window<10224, true, Algo, SinkNt, 2, 16, LdsReader, 1><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
         b, offsets, obase, 0, 0, n, algo, sink_nt);
   }

@@ -16,9 +16,6 @@ struct BucketWs {
   u64 *totalsF;
   uint8_t *ikeys;
   u32 *iidx;
-  // pipelined passes: trash rows, segment descriptors and bucket bases
-  uint8_t *trash;
-  u32 *segdesc, *segrun;
   size_t bytes;
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -72,14 +69,6 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
     off += round256(n * keysize);
     w.iidx = reinterpret_cast<u32 *>(p + off);
     off += round256(n * 4);
-    // pass-2 segments: F * ceil(count-chunks / max(1, F / 8)) <= 8 * count-chunks + F
-    const u64 nseg_max = 8 * tp_chunks + kTpMaxDigits;
-    w.trash = p + off;
-    off += kTrashBytes;
-    w.segdesc = reinterpret_cast<u32 *>(p + off);
-    off += round256(nseg_max * 8);
-    w.segrun = reinterpret_cast<u32 *>(p + off);
-    off += round256(nseg_max * kTpMaxDigits * 4);
   }
   w.bytes = off;
   return w;
@@ -144,94 +133,33 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
 
 
 // Pass 1 and pass 2 each take a shape: W waves x KPL keys per lane per
-// sub-tile, PER_CU workgroups per CU (pass 1: W1, KPL1, PER_CU1).
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int DBG = 0, bool DYN = false,
-          int W1 = W, int KPL1 = KPL, int PER_CU1 = PER_CU, bool PK1 = false>
-static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
-                           u32 *tickets) {
+// sub-tile, PER_CU workgroups per CU (pass 1: W1, KPL1, PER_CU1).  Both run
+// their units in the static XCD-contiguous order (TileOrder; per-XCD tickets
+// gained nothing here, r02 tuning variant 86).
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int W1 = W, int KPL1 = KPL,
+          int PER_CU1 = PER_CU>
+static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
   constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;      // waves per SIMD, pass 2
   constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;  // pass 1
   const size_t b1 = pass1_lds_bytes<W1, KPL1>(), b2 = pass2_lds_bytes<W, KPL>();
-  auto f1 = &k_bucket_pass1<L, W1, KPL1, WPE1, DBG, DYN, PK1>;
-  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, DYN>;
-  auto f1s = &k_bucket_pass1<L, W1, KPL1, WPE1, DBG, false, PK1>;
-  auto f2s = &k_bucket_pass2<L, Out, W, KPL, WPE, DBG, false>;
+  auto f1 = &k_bucket_pass1<L, W1, KPL1, WPE1>;
+  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE>;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
-  if (int rc = set_lds(reinterpret_cast<const void *>(f1s), b1)) return rc;
-  if (int rc = set_lds(reinterpret_cast<const void *>(f2s), b2)) return rc;
   const u64 cus = (u64)std::max(1, g_dev[dev].cus);
   unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU1);
   if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
-  // (tickets need a grid that is a multiple of 8; small grids: static order)
-  if (DYN && g1 % 8 == 0)
-    f1<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp, tickets);
-  else
-    f1s<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp, nullptr);
+  f1<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp);
   unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
   if (g2 >= 8) g2 &= ~7u;
-  if (DYN && g2 % 8 == 0)
-    f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out, tickets + 8);
-  else
-    f2s<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out, nullptr);
+  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out);
   g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
   return 0;
 }
 
-// The pipelined passes (bucket.h k_bucket_pass1_pf / _pass2_pf): 8-B keys,
-// array outputs.  PF1 / PF2 select the pipelined form of each pass (the
-// other runs as launch_two_pass's product shape, 8 x 8 @ 2 / 4 x 8 @ 4);
-// pass 1's DMA pieces need 16-B aligned keys, else it runs the plain form.
-template <bool PF1, int W1, int KPL1, int PC1, bool PF2, int W2, int KPL2, int PC2>
-static int launch_two_pass_pf(const BucketArgs &a, const TwoPass &tp, const OutSoA &out, hipStream_t st, int dev) {
-  constexpr int WPE1 = PC1 * W1 / 4 > 8 ? 8 : PC1 * W1 / 4;
-  constexpr int WPE2 = PC2 * W2 / 4 > 8 ? 8 : PC2 * W2 / 4;
-  const u64 cus = (u64)std::max(1, g_dev[dev].cus);
-  const u32 C4 = (tp.C + 3) & ~3u;
-  if (tp.F < 4 || tp.nseg > 8 * tp.nchunks + kTpMaxDigits)  // dma_row_u32 rows; the workspace's segment tables
-    return fail("pipelined two-pass bucketing: digit split out of range%s", "");
-  if (PF1 && ((uintptr_t)a.k & 15) == 0) {
-    const size_t b1 = pass1_pf_lds_bytes<W1, KPL1>();
-    auto f1 = &k_bucket_pass1_pf<W1, KPL1, WPE1>;
-    if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
-    unsigned g1 = (unsigned)std::min<u64>(tp.ntiles, cus * PC1);
-    if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
-    f1<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp);
-  } else {
-    constexpr int kW = 8, kK = 8, kPc = 2, kWpe = kPc * kW / 4;
-    const size_t b1 = pass1_lds_bytes<kW, kK>();
-    auto f1 = &k_bucket_pass1<8, kW, kK, kWpe, 0, false>;
-    if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
-    unsigned g1 = (unsigned)std::min<u64>(tp.ntiles, cus * kPc);
-    if (g1 >= 8) g1 &= ~7u;
-    f1<<<g1, kW * 64, b1, st>>>(a.k, a.n, a.rk, tp, nullptr);
-  }
-  if (PF2) {
-    const u64 ne = tp.nseg * C4;
-    k_bucket_segdesc<<<(unsigned)((ne + 255) / 256), 256, 0, st>>>(tp, a.nranks, C4);
-    const size_t b2 = pass2_pf_lds_bytes<W2, KPL2>();
-    auto f2 = &k_bucket_pass2_pf<W2, KPL2, WPE2>;
-    if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
-    unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PC2);
-    if (g2 >= 8) g2 &= ~7u;
-    f2<<<g2, W2 * 64, b2, st>>>(a.rk, a.nranks, tp, out, a.n, C4);
-    g_kernel = "k_bucket_pass2_pf<8B>";
-  } else {
-    const size_t b2 = pass2_lds_bytes<kTpW, kTpKPL>();
-    auto f2 = &k_bucket_pass2<8, OutSoA, kTpW, kTpKPL, 4, 0, false>;
-    if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
-    unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * kTpPerCu);
-    if (g2 >= 8) g2 &= ~7u;
-    f2<<<g2, kTpW * 64, b2, st>>>(a.rk, a.nranks, tp, out, nullptr);
-    g_kernel = "k_bucket_pass2<8B>";
-  }
-  return 0;
-}
-
 template <int L, class Out>
-static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev,
-                               u32 *tickets) {
+static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
   // Shapes (waves x keys per lane per sub-tile @ workgroups per CU).  r02's
   // A/B (8 x 4 / 4 x 16 / 4 x 4 keys, 2-6 WG/CU, per-XCD tile tickets) kept
   // 4 x 8 @ 4 for both passes.  r04, interleaved, after the fine-plus digit
@@ -242,43 +170,13 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
   // as well (-9 % at 4096 ranks; 8-B keys +4 % with it).  Pass 2 in 8 x 8 @ 3
   // or 16 x 4 @ 2, pass 1 in 4 x 16 / 16 x 4 / 8 x 4: slower.
 #ifdef PDHT_HIP_TUNING
-  switch (tuning_variant()) {  // r04: the shapes again, per pass, on the fine-plus digit split
-    case 192: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 4, 16, 3>(a, tp, out, st, dev, tickets);
-    case 193: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
-    case 194: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 3>(a, tp, out, st, dev, tickets);
-    case 195: return launch_two_pass<L, Out, 4, 16, 3>(a, tp, out, st, dev, tickets);
-    case 196: return launch_two_pass<L, Out, 8, 8, 2>(a, tp, out, st, dev, tickets);
-    case 197: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 16, 4, 2>(a, tp, out, st, dev, tickets);
-    case 198: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 4, 4>(a, tp, out, st, dev, tickets);
-    case 199: return launch_two_pass<L, Out, 8, 4, 4, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
-    case 200: return launch_two_pass<L, Out, 8, 8, 3, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
-    case 201: return launch_two_pass<L, Out, 16, 4, 2, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
-    case 202: return launch_two_pass<L, Out>(a, tp, out, st, dev, tickets);  // r02-r03: 4 x 8 @ 4 both
-    default: break;
-  }
-  if constexpr (L == 8 && std::is_same<Out, OutSoA>::value) {
-    switch (tuning_variant()) {  // r05: the pipelined passes (pass 1 shape, pass 2 shape)
-      case 230: return launch_two_pass_pf<true, 8, 4, 2, true, 4, 8, 2>(a, tp, out, st, dev);
-      case 231: return launch_two_pass_pf<true, 4, 8, 3, true, 4, 8, 2>(a, tp, out, st, dev);
-      case 232: return launch_two_pass_pf<true, 8, 4, 2, true, 4, 4, 3>(a, tp, out, st, dev);
-      case 233: return launch_two_pass_pf<true, 4, 8, 3, true, 4, 4, 3>(a, tp, out, st, dev);
-      case 234: return launch_two_pass_pf<true, 8, 8, 1, true, 4, 8, 2>(a, tp, out, st, dev);
-      case 235: return launch_two_pass_pf<false, 8, 8, 2, true, 4, 8, 2>(a, tp, out, st, dev);
-      case 236: return launch_two_pass_pf<true, 8, 4, 2, false, 4, 8, 4>(a, tp, out, st, dev);
-      case 237: return launch_two_pass_pf<true, 4, 8, 3, false, 4, 8, 4>(a, tp, out, st, dev);
-      case 238: return launch_two_pass_pf<false, 8, 8, 2, true, 8, 4, 2>(a, tp, out, st, dev);
-      // pass 1 with the packed run table: 8 x 8 at 3 workgroups per CU (LDS 51 KiB each) / at 2
-      case 239: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 3, true>(a, tp, out, st, dev, tickets);
-      case 240: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 2, true>(a, tp, out, st, dev, tickets);
-      case 242: return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 3, true>(a, tp, out, st, dev, tickets);
-      default: break;
-    }
-  }
+  // (r04's shape search, tuning 192-201, removed in r05)
+  if (tuning_variant() == 202) return launch_two_pass<L, Out>(a, tp, out, st, dev);  // r02-r03: 4 x 8 @ 4 both
 #endif
   if constexpr (L == 16)
-    return launch_two_pass<L, Out, 8, 8, 2, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
   else
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 0, false, 8, 8, 2>(a, tp, out, st, dev, tickets);
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
 }
 
 enum class BucketKernel { kStaged, kGeneric, kTwoPass };
@@ -399,9 +297,6 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     tp.fbase = w.fbase;
     tp.ikeys = w.ikeys;
     tp.iidx = w.iidx;
-    tp.trash = w.trash;
-    tp.segdesc = w.segdesc;
-    tp.segrun = w.segrun;
     tp.ntiles = ntiles;
     tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
     tp.SG = std::max<u64>(1, (u64)tp.F * kTpSegKeys / ((u64)kTpChunkTiles * kTpCountTile));  // ~kTpSegKeys keys
@@ -411,14 +306,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   if (ntiles && kind == BucketKernel::kTwoPass) {
     const u64 nchunks32 = (ntiles + kBucketChunk - 1) / kBucketChunk;
     const unsigned gc = (unsigned)std::min<u64>(tp.nchunks, (u64)std::max(1, g_dev[dev].cus) * 8);
-    bool count_pf = false;
-#ifdef PDHT_HIP_TUNING
-    count_pf = tuning_variant() == 241 || tuning_variant() == 242;  // r05: next tile's keys loaded ahead
-#endif
-    if (keysize == 8 && count_pf)
-      k_bucket_count_tp<8, true><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                                ntiles);
-    else if (keysize == 8)
+    if (keysize == 8)
       k_bucket_count_tp<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
                                                           ntiles);
     else if (keysize == 16)
@@ -463,9 +351,9 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     else
 #endif
     if (kind == BucketKernel::kTwoPass)
-      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev, w.tickets)
-           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev, w.tickets)
-                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev, w.tickets);
+      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev)
+           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev)
+                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev);
     else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner8x16)
       rc = keysize == 8    ? launch_staged<8, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)

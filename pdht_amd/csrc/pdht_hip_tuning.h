@@ -13,7 +13,10 @@ extern "C" {
 #endif
 
 /* Select an alternative kernel where one exists (0 = the product's choice).
- * Every variant the sources know (DESIGN.md §4 has the measurements):
+ * The alternatives live in pdht_amd/csrc/tuning/ (kernels_tuning.h,
+ * launch_tuning.h) and the tuning hooks of the C-ABI sources; the product
+ * headers hold only what ships.  Every variant the sources know (DESIGN.md
+ * §4 has the measurements):
  *   64-B keys      7  one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
  *                 26  plain instead of non-temporal digest stores (2-6 % slower)
  *                188  digests stored 16 B per lane (even lanes, DPP pairs: Sink64x2T)
@@ -58,12 +61,11 @@ extern "C" {
  *                 71  two passes from 2 ranks up
  *              83/87  owner-table ranking on 8 x 16 / 4 x 16 tiles, any nranks
  *              85/89  ballot ranking, any nranks (85: static tile order)
- *            192-196  two-pass sub-tile shapes (waves x keys per lane @ WG/CU): pass 1
- *                     4x16@3 / 8x8@2 / 8x8@3 (pass 2 as shipped); both passes
- *                     4x16@3 / 8x8@2 (product: 4x8@4 for both); 197/198 pass 1
- *                     16x4@2 / 8x4@4; 199-201 pass 1 8x8@2 with pass 2 8x4@4 /
- *                     8x8@3 / 16x4@2; 202 the r02-r03 shape (4x8@4 both passes;
- *                     product since r04: pass 1 8x8@2, pass 2 4x8@4 (16-B keys 8x8@2))
+ *                202  the r02-r03 two-pass sub-tile shape (4 x 8 @ 4 for both passes;
+ *                     product since r04: pass 1 8x8@2, pass 2 4x8@4 (16-B keys 8x8@2));
+ *                     r04's other shapes (192-201) and r05's LDS-DMA pipelined passes,
+ *                     packed pass-1 tables and prefetching count kernel (230-242) were
+ *                     measured slower and removed
  *                164  two-pass arrays of 8/16-B keys on the balanced digit split
  *                     F = 2^ceil(nbits/2) (product: one fine bit more)
  *   records      112  r02 store order (header halves a staging round early)

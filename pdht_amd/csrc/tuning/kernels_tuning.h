@@ -1,0 +1,290 @@
+// tuning/kernels_tuning.h -- the TUNING build's alternative kernels, readers,
+// sinks and algorithms (libpdht_hip_tuning.so, -DPDHT_HIP_TUNING; used by
+// tools/abbench.py and the `--tuning` GPU tests only, never by the product
+// library).  Each was measured against the product form and lost, or is a
+// calibration (a kernel with part of its work removed, wrong digests) that
+// DESIGN.md §4 quotes; the product headers (kernels.h, bucket.h) hold only
+// what ships.  Included by tuning/launch_tuning.h and the tuning hooks of the
+// C-ABI sources.
+#pragma once
+#include "../kernels.h"
+
+namespace pdht {
+
+// Key bytes in LDS at an arbitrary byte offset, r01-r03 form (tuning variant
+// 175 now): a span of N bytes is one run of N/4+1 dword reads from one base
+// address (ds_read2_b32 with immediate offsets, a single wait) funnelled by
+// v_alignbyte_b32; the window carries 16 B of slack so the trailing dword
+// read stays in the array.
+struct LdsReaderFunnel {
+  const u32 *lds;
+  u32 base;
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> span(u32 o) const {
+    const u32 a = base + o;
+    const u32 *p = lds + (a >> 2);
+    const u32 r = a & 3u;
+    u32 raw[N / 4 + 1];
+#pragma unroll
+    for (int j = 0; j <= N / 4; ++j) raw[j] = p[j];
+    Words<N / 4> w;
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) w.d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], r);
+    return w;
+  }
+  __device__ __forceinline__ u32 w32(u32 o) const { return span<4>(o).d[0]; }
+  __device__ __forceinline__ u32 b8(u32 o) const {
+    const u32 a = base + o;
+    return (lds[a >> 2] >> (8 * (a & 3u))) & 0xffu;
+  }
+};
+
+// r02's 6-bit-slice CRC-32C tables (tuning variant 150): 11 x 64 entries =
+// 2816 B; a 64-word table covers each of the 64 banks once, so random
+// indices stay conflict-free, at 11 lookups per word against 8.
+struct CrcLds6Tab {
+  const u32 *t;  // [11][64]
+  __device__ __forceinline__ u32 crc64(u64 x) const {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    u32 r = t[0 * 64 + (lo & 63)] ^ t[1 * 64 + ((lo >> 6) & 63)] ^ t[2 * 64 + ((lo >> 12) & 63)] ^
+            t[3 * 64 + ((lo >> 18) & 63)] ^ t[4 * 64 + ((lo >> 24) & 63)];
+    r ^= t[5 * 64 + (__builtin_amdgcn_alignbit(hi, lo, 30) & 63)];
+    r ^= t[6 * 64 + ((hi >> 4) & 63)] ^ t[7 * 64 + ((hi >> 10) & 63)] ^ t[8 * 64 + ((hi >> 16) & 63)] ^
+         t[9 * 64 + ((hi >> 22) & 63)] ^ t[10 * 64 + (hi >> 28)];
+    return r;
+  }
+};
+
+template <>
+struct CrcLdsSlices<6> {
+  typedef CrcLds6Tab Tab;
+  static constexpr u32 kWords = 11 * 64;
+  __device__ static void fill(u32 *tab) {
+    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = kCrc6Dev.t[k >> 6][k & 63];
+  }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
+};
+
+// Timing only: the CRC-32C of a word replaced by a fold (no table lookups):
+// what the lookups cost the long-key kernel (wrong digests).
+struct CrcNullTab {
+  const u32 *t;
+  __device__ __forceinline__ u32 crc64(u64 x) const { return (u32)x ^ (u32)(x >> 32) ^ t[0]; }
+};
+
+template <>
+struct CrcLdsSlices<0> {  // CrcNullTab: the 6-bit form's launch shape, no lookups
+  typedef CrcNullTab Tab;
+  static constexpr u32 kWords = 64;
+  __device__ static void fill(u32 *tab) {
+    for (u32 k = threadIdx.x; k < kWords; k += blockDim.x) tab[k] = 0;
+  }
+  __device__ __forceinline__ static Tab make(const u32 *t) { return Tab{t}; }
+};
+
+// Tuning-only calibrations of the variable-length window kernel: the digest
+// is the key length (no key byte is read from LDS), so the kernel is its
+// window DMA, offsets loads and digest stores alone.
+struct AlgoLenOnly {
+  typedef u64 Out;
+  template <class R>
+  __device__ __forceinline__ Out operator()(const R &, u64 len) const {
+    return len;
+  }
+};
+// Timing only: CityHash64 twice per key (the second over the key minus its
+// first byte), to see what the hash arithmetic itself costs a kernel.
+struct AlgoCity64x2 {
+  typedef u64 Out;
+  template <class R>
+  __device__ __forceinline__ Out operator()(const R &r, u64 len) const {
+    return city64(r, len) ^ (len ? city64(Shifted<R>{r, 1u}, len - 1) : 0);
+  }
+};
+
+// 64-bit digests stored 16 B per lane: every even lane takes its odd
+// neighbour's digest (two DPP row_shl:1 moves) and stores both with one
+// dwordx4, so a wave's 512 B of digests leave as 32 lane-stores instead of
+// 64 (i must be 64-aligned tile base + lane, as in every kernel here; a lane
+// whose partner is inactive -- past the batch's end, or in another branch of
+// a divergent hash -- stores its own digest alone).
+template <bool NTS = true>
+struct Sink64x2T {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64 i, u64 h) {
+    const u32 lo = (u32)h, hi = (u32)(h >> 32);
+    const u32 lo1 = __builtin_amdgcn_mov_dpp(lo, 0x101, 0xf, 0xf, false);  // row_shl:1: lane l <- l+1
+    const u32 hi1 = __builtin_amdgcn_mov_dpp(hi, 0x101, 0xf, 0xf, false);
+    const u32 lane = (u32)i & 63;
+    // partner = the other lane of the pair; the two may sit in different
+    // divergent branches (then each stores its own digest)
+    const bool partner = (__builtin_amdgcn_read_exec() >> (lane ^ 1)) & 1;
+    if ((lane & 1) == 0 && partner)
+      st<NTS>(u32x4{lo, hi, lo1, hi1}, reinterpret_cast<u32x4 *>(out + i));
+    else if (!partner)
+      st<NTS>(h, out + i);
+  }
+  __device__ __forceinline__ void flush() {}
+  __host__ Sink64x2T shift(u64 k0) const { return Sink64x2T{lds_hist, out + k0}; }
+};
+
+// Calibration only: digests dropped (a kernel's loads alone).
+struct SinkNone {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64, u64 h) {
+    if (h == 0x0123456789abcdefull) out[0] = h;  // keeps the digest live, never taken
+  }
+  __device__ __forceinline__ void flush() {}
+};
+// Calibration only: every digest stored, but into the first 32 KiB of out
+// (L2-resident): the store instructions without their HBM writes.
+struct SinkSmall {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64 i, u64 h) { out[i & 4095] = h; }
+  __device__ __forceinline__ void flush() {}
+};
+// Calibration only: nt digest stores wrapped into the first 2^BITS digests
+// of out (2^BITS x 8 B: L2-sized to Infinity-Cache-sized destinations).
+template <int BITS>
+struct SinkRing {
+  static constexpr u32 kHist = 1;
+  u32 *lds_hist;
+  u64 *out;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void put(u64 i, u64 h) { st<true>(h, out + (i & ((1ull << BITS) - 1))); }
+  __device__ __forceinline__ void flush() {}
+  __host__ SinkRing shift(u64) const { return *this; }
+};
+
+// ------------------------------------------------ pipelined window kernel ---
+// Offset-indexed keys with 64-bit digests, one LDS window per wave as in
+// k_window, but with every memory latency except the window DMA's taken off a
+// tile's critical path.  k_window's tile is a chain of four dependent memory
+// round trips -- offsets (a vmcnt(0) wait that also waits for the previous
+// tile's digest store to be acknowledged), two scalar loads of the window
+// bounds, then the DMA.  Here:
+//   * the offsets of the wave's next tile are loaded while this tile's window
+//     streams in: one dwordx4 per lane = offsets[i], offsets[i+1] (index
+//     clamped to n-1, so the load is always issued and the clamped lanes read
+//     offsets[n]); the window is [lane 0's start, lane 63's end) by readlane --
+//     no scalar loads, whose lgkmcnt wait would meet the LDS reads;
+//   * a tile's digests are stored one tile late, right after the next tile's
+//     DMA and offsets load are issued, as a raw buffer store whose range
+//     check drops the lanes past n (always issued, even with no valid lane);
+//   * so the wait for a window is s_waitcnt vmcnt(2): on gfx950 loads, stores
+//     and LDS-DMA count together in issue order (MI355X_MICROARCH.md,
+//     "s_waitcnt vmcnt(N)"), and the two youngest operations are exactly that
+//     offsets load and that store -- the wait never includes a store.
+// G = tiles a wave takes in a row before jumping by the grid (1: the grid
+// stride of k_window; 16: r02's grouped order, consecutive windows per wave).
+// RING (calibration only): digests of tile t go to out + 64 * (t % RING), an
+// L2-resident destination -- the kernel without its HBM writes.
+// SAUX: cache-policy bits of the digest stores (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
+template <int WIN, int G, class Algo, int AUX = 2, class LR = LdsReader, u64 RING = 0, int SAUX = AUX>
+__global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restrict__ bytes,
+                                                        const u64 *__restrict__ offsets, u64 obase, u64 n,
+                                                        Algo algo, u64 *__restrict__ out) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
+  algo_init(algo);
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) >> 6;
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  u32 *lds = win_all + wave * (WIN / 4);
+  const u64 base = (u64)(uintptr_t)bytes;
+  // tile order: runs of G consecutive tiles, run r of wave w = gw + r * nwaves
+  const u64 gw = (u64)blockIdx.x * kWavesPerBlock + wave;
+  auto next = [&](u64 t) -> u64 {
+    if (G > 1 && (t + 1) % G != 0) return t + 1;
+    return (t / G + nwaves) * G;
+  };
+  u64 t = gw * G;
+  if (t >= ntiles) return;
+  // key i's bounds: offsets[min(i, n-1)] and the next entry (n >= 1 here)
+  auto bounds = [&](u64 tt, u64 &a, u64 &e) {
+    const u64 *p = offsets + ((tt << 6) + lane < n ? (tt << 6) + lane : n - 1);
+    a = p[0];
+    e = p[1];
+  };
+  auto rd64 = [](u64 v, u32 l) -> u64 {
+    return (u64)(u32)__builtin_amdgcn_readlane((u32)v, l) |
+           ((u64)(u32)__builtin_amdgcn_readlane((u32)(v >> 32), l) << 32);
+  };
+  u64 a, e;
+  bounds(t, a, e);
+  u64 hprev = 0, tprev = ~0ull;  // digest of the previous tile (none yet)
+  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+  while (true) {
+    const u64 k0 = t << 6;
+    const u64 i = k0 + lane;
+    const bool valid = i < n;
+    const u64 start = a - obase;
+    const u64 end = e - obase;
+    const u64 first = rd64(a, 0) - obase;
+    const u64 whi = rd64(e, 63) - obase;
+    const u64 wlo = (base + first) & ~(u64)15;  // absolute, as in k_window
+    const u64 span = whi > first ? base + whi - wlo : 0;
+    const u32 wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)wlo);
+#pragma unroll
+    for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
+      if ((u32)j * 1024 < wbytes) {  // wave-uniform
+        if ((u32)j * 1024 + lane * 16 < wbytes)
+          __builtin_amdgcn_global_load_lds(
+              (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+              (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, AUX);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the next tile's offsets (always issued: clamped index; past the end the
+    // loop stops before they are used)
+    const u64 tn = next(t);
+    u64 an, en;
+    bounds(tn, an, en);
+    __builtin_amdgcn_sched_barrier(0);
+    // the previous tile's digests (always issued; records past n dropped)
+    {
+      const u64 pk = tprev << 6;
+      const u32 nrec = tprev == ~0ull ? 0u : (u32)((n - pk < 64 ? n - pk : 64) * 8);
+      const u64 dst = tprev == ~0ull ? 0 : RING ? (tprev % RING) << 6 : pk;
+      __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + dst, 0, nrec, 0x00020000);
+      const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+      const u64 len = end - start;
+      if (base + end - wlo <= wbytes)
+        hprev = algo(LR{lds, (u32)(base + start - wlo)}, len);
+      else
+        hprev = algo(GlobalReader{bytes + start}, len);
+    }
+    tprev = t;
+    __builtin_amdgcn_wave_barrier();  // window reused by the next tile
+    if (tn >= ntiles) break;
+    t = tn;
+    a = an;
+    e = en;
+  }
+  // the last tile's digests
+  const u64 pk = tprev << 6;
+  const u32 nrec = (u32)((n - pk < 64 ? n - pk : 64) * 8);
+  __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(out + (RING ? (tprev % RING) << 6 : pk), 0, nrec, 0x00020000);
+  const u32x2 w = {(u32)hprev, (u32)(hprev >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
+}
+
+}  // namespace pdht

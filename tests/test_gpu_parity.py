@@ -134,12 +134,13 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
 
 
 @pytest.mark.tuning
+@pytest.mark.parametrize("variant", [150])
 @pytest.mark.parametrize("L", [901, 1024, 2200])
-def test_crc128_long_keys_6bit_tables(dev, oracle, L):
+def test_crc128_long_keys_6bit_tables(dev, oracle, L, variant):
     """Tuning variant 150: the long-key CRC-32C on r02's 6-bit-slice tables."""
     rng = np.random.default_rng(L + 5)
     k = rng.integers(0, 256, (20_001, L), dtype=np.uint8)
-    with P.tuning(150):
+    with P.tuning(variant):
         got = u64(P.citycrc128_batch(to_dev(k, dev)))
     assert (got == oracle.city128_fixed(k, crc=True)).all()
 
@@ -527,23 +528,14 @@ BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535
 BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
                  for nr in (1, 7, 511, 512, 1000, 1462, 1463, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
-# 192-196: two-pass sub-tile shapes per pass (r04)
-BUCKET_CASES += [(L, nr, n, v) for v in range(192, 203) for L in (8, 16, 32) for nr in (2049, 8192)
+# 202: the r03 two-pass sub-tile shape (4 x 8 @ 4 for both passes)
+BUCKET_CASES += [(L, nr, n, v) for v in (202,) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
 # 164: two-pass arrays on the balanced digit split (the product takes one fine bit more)
 BUCKET_CASES += [(L, nr, n, 164) for L in (8, 16, 32) for nr in (1025, 2049, 4097, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
 # the product's fine-plus split at its edges: 71 forces two passes from 2 ranks (nbits 1..3)
 BUCKET_CASES += [(L, nr, 70001, 71) for L in (8, 32) for nr in (2, 3, 4, 5, 8, 9)]
-# 230-238 (r05): the LDS-DMA pipelined passes (8-B keys, array outputs) in
-# several shapes; ragged sizes end in partial sub-tiles and segments
-PF_VARIANTS = tuple(range(230, 239))
-BUCKET_CASES += [(8, nr, n, v) for v in PF_VARIANTS for nr in (1536, 2047, 4097, 8192)
-                 for n in (1, 4095, 12288, 300007, (1 << 20) + 5, (4 << 20) + 3)]
-# 239-242 (r05): pass 1 on a packed run table at 3 / 2 workgroups per CU, the
-# two-pass count kernel loading the next tile ahead (241; 242 = both)
-BUCKET_CASES += [(8, nr, n, v) for v in (239, 240, 241, 242) for nr in (1536, 4097, 8192)
-                 for n in (1, 4095, 300007, (1 << 20) + 5, (4 << 20) + 3)]
 
 
 def _bucket_kernel(L, nranks, variant, records=False):
@@ -561,8 +553,6 @@ def _bucket_kernel(L, nranks, variant, records=False):
         two_pass_from = {8: 1536, 16: 1025, 32: 2049}[L]
         one_pass = variant == 70 and nranks <= 2048
         if (variant == 71 and nranks >= 2) or (not one_pass and nranks >= two_pass_from):
-            if L == 8 and not records and variant in PF_VARIANTS and variant not in (236, 237):
-                return "k_bucket_pass2_pf<8B>"
             return f"k_bucket_pass2<{L}B>"
         # staged_shape(): owner-table ranking for array outputs from 512
         # ranks, on 8 x 16 tiles for 8/16-B keys while 81920 + 52 B per rank
@@ -626,44 +616,6 @@ def test_bucket_skewed(dev, oracle, L, nranks, variant):
     assert (ko.cpu().numpy() == k[order]).all()
     want_offs = np.concatenate([[0], np.cumsum(np.bincount(r2, minlength=nranks))])
     assert (offs.cpu().numpy() == want_offs).all()
-
-
-@pytest.mark.tuning
-@pytest.mark.parametrize("variant", [230, 231, 233])
-@pytest.mark.parametrize("nranks", [2047, 8192])
-def test_bucket_pf_outputs_and_alignment(dev, oracle, variant, nranks):
-    """The pipelined passes with each optional output omitted (a wave's
-    store count per sub-tile changes with them), on keys 8-B but not 16-B
-    aligned (pass 1 then runs its plain form) and on a skewed batch (segments
-    of many sub-tiles, empty segments)."""
-    rng = np.random.default_rng(nranks + variant)
-    n = 700_001
-    k = rng.integers(0, 256, (n, 8), dtype=np.uint8)
-    buf = torch.zeros((n + 1) * 8, dtype=torch.uint8, device=dev)
-    buf[8:].copy_(to_dev(k.reshape(-1), dev))
-    kd_mis = buf[8:].view(n, 8)  # 8 B past a 256-B aligned allocation
-    assert kd_mis.data_ptr() % 16 == 8
-    m2, p2, r2 = oracle.pdht_hash_fixed(k, 3, nranks)
-    order = np.argsort(r2, kind="stable")
-    with P.tuning(variant):
-        for kd in (to_dev(k, dev), kd_mis):
-            for wk, wp, wi in ((True, True, True), (False, False, True), (True, False, False), (False, True, False)):
-                ko, mb, pt, ix, offs = P.bucket_batch(kd, 3, nranks, with_keys=wk, with_ptindex=wp, with_index=wi)
-                assert P.last_kernel() == "k_bucket_pass2_pf<8B>"
-                assert (u64(mb) == m2[order]).all()
-                if ix is not None:
-                    assert (ix.cpu().numpy().view(np.uint32) == order).all()
-                if pt is not None:
-                    assert (pt.cpu().numpy().view(np.uint32) == p2[order]).all()
-                if ko is not None:
-                    assert (ko.cpu().numpy() == k[order]).all()
-        distinct = rng.integers(0, 256, (3, 8), dtype=np.uint8)
-        ks = distinct[rng.integers(0, 3, n)]
-        ko, mb, pt, ix, offs = P.bucket_batch(to_dev(ks, dev), 3, nranks)
-    m3, _, r3 = oracle.pdht_hash_fixed(ks, 3, nranks)
-    o3 = np.argsort(r3, kind="stable")
-    assert (ix.cpu().numpy().view(np.uint32) == o3).all() and (u64(mb) == m3[o3]).all()
-    assert (ko.cpu().numpy() == ks[o3]).all()
 
 
 @pytest.mark.parametrize("L", [8, 16, 13])

@@ -61,6 +61,12 @@ for step in "$@"; do
     rehearse2) # the N = 2 path end to end on one GPU: 2 ranks, gloo collectives, both ranks on device 0
              timeout -k 10 500 python bench.py --gpus 2 --dist-backend gloo > gpurun_out/rehearse2.log 2>&1; rc=$?
              tail -1 gpurun_out/rehearse2.log | cut -c1-900 ;;
+    rehearse2_*) cfg=${step#rehearse2_}  # the N = 2 gloo rehearsal of another config
+             timeout -k 10 500 python bench.py --gpus 2 --dist-backend gloo --config $cfg > "gpurun_out/$step.log" 2>&1; rc=$?
+             tail -1 "gpurun_out/$step.log" | cut -c1-900 ;;
+    clk_*)   cfg=${step#clk_}  # per-dispatch clock: GRBM_GUI_ACTIVE cycles over the traced duration
+             timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/clk_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps ${STEPS:-50} --warmup ${WARM:-10} --no-cpu-baseline --no-host > gpurun_out/clk_$cfg.log 2>&1; rc=$?
+             tail -1 gpurun_out/clk_$cfg.log | cut -c1-300 ;;
     rehearse4) # N = 4 the same way: 4 ranks on device 0 (configs[4] = 4 x 256M keys)
              timeout -k 10 800 python bench.py --gpus 4 --dist-backend gloo > gpurun_out/rehearse4.log 2>&1; rc=$?
              tail -1 gpurun_out/rehearse4.log | cut -c1-1500 ;;
