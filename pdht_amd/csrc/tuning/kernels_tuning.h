@@ -287,4 +287,144 @@ __global__ __launch_bounds__(kBlock) void k_window_pipe(const uint8_t *__restric
   __builtin_amdgcn_raw_buffer_store_b64(w, r, lane * 8, 0, SAUX);
 }
 
+// ------------------------------------------------ 64-B tile-order probe ---
+// k_fixed_xpose64 (kernels.h) with the wave -> tile order as a parameter
+// (r05 experiment on the allocation-dependent speed of the 64-B stream,
+// DESIGN.md §4.1): ORDER 1 = tile t at position (t * 0x9E3779B1) mod ntiles
+// (ntiles a power of two: a bijection that scatters the tiles in flight over
+// the whole batch instead of one contiguous window); ORDER 2 = each wave a
+// contiguous run of ceil(ntiles / nwaves) tiles.
+// Digests go where their keys' tile is.
+template <class Algo, class Sink, int ORDER>
+__global__ __launch_bounds__(kBlock) void k_fixed_xpose64_order(const uint8_t *__restrict__ keys, u64 n, Algo algo,
+                                                                Sink sink) {
+  constexpr int DEPTH = 2;
+  __shared__ __attribute__((aligned(16))) u32x4 img[kWavesPerBlock][256];
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 ntiles = n >> 6;  // the launcher passes whole tiles only
+  const u64 nwaves = (u64)gridDim.x * kWavesPerBlock;
+  const u64 gw = (u64)blockIdx.x * kWavesPerBlock + wave;
+  const u64 per = (ntiles + nwaves - 1) / nwaves;  // ORDER 2: tiles per wave (the last waves fewer)
+  // k-th tile of this wave (k = 0, 1, ...) -> physical tile
+  auto tile = [&](u64 k) -> u64 {
+    if constexpr (ORDER == 2) return gw * per + k;
+    const u64 t = gw + k * nwaves;
+    return ORDER == 1 ? (t * 0x9E3779B1ull) & (ntiles - 1) : t;
+  };
+  const u64 nk = ORDER == 2 ? (gw * per < ntiles ? min(per, ntiles - gw * per) : 0)
+                            : (ntiles > gw ? (ntiles - gw + nwaves - 1) / nwaves : 0);
+  u32x4 pre[DEPTH][4];
+  auto fetch = [&](int d, u64 t) {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(keys + (t << 12));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pre[d][j] = ld<true>(src + 64 * j + lane);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if ((u64)d < nk) fetch(d, tile(d));
+  for (u64 k = 0; k < nk; k += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      if (k + d >= nk) break;  // wave-uniform
+      const u64 tt = tile(k + d);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32 g = 64 * j + lane;
+        img[wave][xpose_slot(g >> 2, g & 3)] = pre[d][j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (k + d + DEPTH < nk) fetch(d, tile(k + d + DEPTH));
+      RegReader<16> r;
+      const u32 sw = (lane >> 2) & 3;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const u32x4 v = img[wave][4 * lane + (c ^ sw)];
+        r.d[4 * c + 0] = v.x;
+        r.d[4 * c + 1] = v.y;
+        r.d[4 * c + 2] = v.z;
+        r.d[4 * c + 3] = v.w;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      sink.put((tt << 6) + lane, algo(r, (u64)64));
+    }
+  }
+  sink.flush();
+}
+
+// ------------------------------------- workgroup write-combined window ---
+// k_window for offset-indexed keys with 64-bit
+// digests, where the 4 waves of a workgroup take 4 CONSECUTIVE tiles (a
+// 256-key super-tile), stage their digests in LDS and the workgroup stores
+// the super-tile's 2 KiB of digests as one contiguous run (256 threads x 8 B,
+// non-temporal), instead of each wave storing its own 512 B when its tile is
+// done.  Two barriers per super-tile couple the 4 waves.
+template <int WIN, class Algo>
+__global__ __launch_bounds__(kBlock) void k_window_wc(const uint8_t *__restrict__ bytes,
+                                                      const u64 *__restrict__ offsets, u64 obase, u64 n, Algo algo,
+                                                      u64 *__restrict__ out) {
+  static_assert(WIN % 16 == 0, "window = whole 16-B DMA lanes");
+  __shared__ __attribute__((aligned(16))) u32 win_all[kWavesPerBlock * (WIN / 4) + 4];
+  __shared__ u64 dig[kBlock];
+  algo_init(algo);
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lane = threadIdx.x & 63;
+  const u64 nsuper = (n + kBlock - 1) / kBlock;
+  u32 *lds = win_all + wave * (WIN / 4);
+  const u64 base = (u64)(uintptr_t)bytes;
+  for (u64 sp = blockIdx.x; sp < nsuper; sp += gridDim.x) {
+    __builtin_amdgcn_s_setprio(1);
+    const u64 k0 = sp * kBlock + wave * 64;  // this wave's tile
+    const u64 i = k0 + lane;
+    const bool valid = i < n;
+    u64 start = 0, end = 0;
+    if (valid) {
+      start = offsets[i] - obase;
+      end = offsets[i + 1] - obase;
+    }
+    u32 wbytes = 0;
+    u64 wlo = 0;
+    if (k0 < n) {
+      const u64 kend = (k0 + 64 < n) ? k0 + 64 : n;
+      const u64 whi = offsets[kend] - obase;
+      const u64 first = offsets[k0] - obase;
+      wlo = (base + first) & ~(u64)15;
+      const u64 span = whi > first ? base + whi - wlo : 0;
+      wbytes = span < (u64)WIN ? (u32)span : (u32)WIN;
+      const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)wlo);
+#pragma unroll
+      for (int j = 0; j < (WIN + 1023) / 1024; ++j) {
+        if ((u32)j * 1024 < wbytes) {
+          if ((u32)j * 1024 + lane * 16 < wbytes)
+            __builtin_amdgcn_global_load_lds(
+                (const void __attribute__((address_space(1))) *)(src + j * 1024 + lane * 16),
+                (void __attribute__((address_space(3))) *)(lds + 256 * j), 16, 0, 2);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    u64 h = 0;
+    if (valid) {
+      const u64 len = end - start;
+      if (base + end - wlo <= wbytes)
+        h = algo(LdsReader{lds, (u32)(base + start - wlo)}, len);
+      else
+        h = algo(GlobalReader{bytes + start}, len);
+    }
+    dig[threadIdx.x] = h;
+    __syncthreads();
+    const u64 j = sp * kBlock + threadIdx.x;
+    if (j < n) __builtin_nontemporal_store(dig[threadIdx.x], out + j);  // the super-tile's 2 KiB in one run
+    __syncthreads();  // windows and dig reused by the next super-tile
+  }
+}
+
 }  // namespace pdht

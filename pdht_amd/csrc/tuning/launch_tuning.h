@@ -7,7 +7,8 @@
 //   64-B keys    7 one tile of prefetch per wave at 4 WG/CU; 26 plain digest
 //                stores; 80 / 81 1024-thread transpose at 1 / 2 WG/CU; 82 the
 //                256-thread shape whatever the histogram; 188 digests stored
-//                16 B per lane; 206 s_setprio 1 around the prefetch issue
+//                16 B per lane; 206 s_setprio 1 around the prefetch issue;
+//                250 / 251 the tile order scattered / in per-wave runs
 //   small keys   219 / 220 8-B placement with 4 / 16 keys per lane in flight;
 //                221 8-B hashing with plain loads; 222 / 223 8 keys per lane
 //                (256 / 1024 threads); 224 32-B keys with plain loads and
@@ -18,7 +19,8 @@
 //   var keys     12 / 13 force the 10224-B / 16-KiB window; 170-173 the
 //                pipelined window kernel; 174 / 175 the r03 funnel reader;
 //                180-187 the pipelined kernel's cache policies; 189 16-B
-//                digest stores; 203 / 204 s_setprio 3 / 1; 205 no s_setprio
+//                digest stores; 203 / 204 s_setprio 3 / 1; 205 no s_setprio;
+//                252 workgroup-combined digest stores (2 KiB runs)
 #pragma once
 #include "kernels_tuning.h"
 
@@ -135,6 +137,21 @@ static int tuning_xpose64(const uint8_t *k, size_t n, Algo algo, Sink sink, hipS
         return tuning_launched();
       }
       return kNoVariant;
+    case 250:
+    case 251: {  // r05: scattered (power-of-two tile counts) / wave-contiguous tile order, whole tiles
+      const u64 ntiles = n >> 6;
+      const unsigned g = grid_for((n + 255) / 256, 3, dev);
+      if (n % 64 || ntiles == 0) return kNoVariant;
+      if (tuning_variant() == 250 && (ntiles & (ntiles - 1))) return kNoVariant;
+      if (tuning_variant() == 250) {
+        g_kernel = "k_fixed_xpose64_order<scatter>@3";
+        k_fixed_xpose64_order<Algo, SinkNt, 1><<<g, kBlock, 0, st>>>(k, n, algo, sink_nt);
+      } else {
+        g_kernel = "k_fixed_xpose64_order<runs>@3";
+        k_fixed_xpose64_order<Algo, SinkNt, 2><<<g, kBlock, 0, st>>>(k, n, algo, sink_nt);
+      }
+      return tuning_launched();
+    }
     case 26:  // plain digest stores (r01: 2-6 % slower)
       g_kernel = "k_fixed_xpose64<nt-load,plain-store,d2>@3";
       k_fixed_xpose64<Algo, Sink, true, 2><<<grid_for((n + 255) / 256, 3, dev), kBlock, 0, st>>>(k, n, algo, sink);
@@ -213,6 +230,12 @@ static int tuning_var(const uint8_t *b, const u64 *offsets, u64 obase, size_t n,
       else
         k_window<10224, true, Algo, Sink64T<true>, 2, 16, LdsReader, 1><<<grid_for(wb, 4, dev), kBlock, 0, st>>>(
             b, offsets, obase, 0, 0, n, algo, Sink64T<true>{nullptr, sink.out});
+      return tuning_launched();
+    }
+    if (v == 252 && !wide) {  // r05: workgroup-combined digest stores (super-tiles of 4 consecutive tiles)
+      g_kernel = "k_window_wc<var,10224>@4";
+      k_window_wc<10224, Algo><<<grid_for(((n + 63) / 64 + 3) / 4, 4, dev), kBlock, 0, st>>>(b, offsets, obase, n,
+                                                                                          algo, sink.out);
       return tuning_launched();
     }
     if (v == 189) {  // the product window kernel, digests stored 16 B per lane

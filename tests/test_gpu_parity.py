@@ -195,6 +195,19 @@ VARIANT_KERNELS = {0: "k_fixed_xpose64<nt,d2>@3", 7: "k_fixed_xpose64<nt,d1>@4",
                    26: "k_fixed_xpose64<nt-load,plain-store,d2>@3"}
 
 
+@pytest.mark.tuning
+@pytest.mark.parametrize("variant,n", [(250, 1 << 20), (250, 64), (251, 1 << 20), (251, 3 * (1 << 18) + 64 * 5)])
+def test_64B_tile_order_probe(dev, oracle, variant, n):
+    """Tuning 250 / 251 (r05): the 64-B kernel with the tile order scattered
+    over the batch / in per-wave contiguous runs (whole tiles only)."""
+    k = oracle.fixed_keys(n, 64)
+    with P.tuning(variant):
+        got = u64(P.city64_batch(to_dev(k, dev)))
+        kern = P.last_kernel()
+    assert kern == ("k_fixed_xpose64_order<scatter>@3" if variant == 250 else "k_fixed_xpose64_order<runs>@3")
+    assert (got == oracle.city64_fixed(k)).all()
+
+
 @pytest.mark.parametrize("variant", _variants(sorted(VARIANT_KERNELS)))
 def test_64B_kernel_variants_bitexact(dev, oracle, variant):
     """The product kernel, and the tuning build's alternatives (A/B only)."""
@@ -308,6 +321,19 @@ VAR_KERNELS = {0: "auto", 12: "k_window<var,nt,10224>@4", 13: "k_window<var,nt,1
                174: "k_window_pipe<var,10224,G1,funnel>@4", 175: "k_window<var,nt,10224,funnel>@4",
                189: "k_window<var,nt,10224,st16>@4", 203: "k_window<var,nt,10224,prio3>@4",
                204: "k_window<var,nt,10224,prio1>@4", 205: "auto"}  # 205: the product's choice, no s_setprio
+
+
+@pytest.mark.tuning
+@pytest.mark.parametrize("n", [1, 63, 64, 255, 256, 257, 100003, (1 << 20) + 7])
+def test_var_wc_kernel(dev, oracle, n):
+    """Tuning 252 (r05): the window kernel with workgroup-combined digest
+    stores (4 consecutive tiles per workgroup, one 2 KiB store run)."""
+    data, offs = oracle.mixed_keys(n)
+    with P.tuning(252):
+        got = u64(P.city64_var_batch(to_dev(data, dev), to_dev(offs.astype(np.int64), dev)))
+        if data.size // n <= 160:  # (wider batches take the 16 KiB window kernel)
+            assert P.last_kernel() == "k_window_wc<var,10224>@4"
+    assert (got == oracle.city64_var(data, offs)).all()
 
 
 def auto_var_kernel(total_bytes, n):

@@ -40,12 +40,18 @@ for step in "$@"; do
     prof_*)  cfg=${step#prof_}; d="gpurun_out/$step"
              timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$d" -o run --output-format csv -- python3 bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline --no-host > "$d.log" 2>&1; rc=$?
              python3 -c "import csv,sys; [print(r['Name'][:90], r['Calls'], r['AverageNs']) for r in csv.DictReader(open(sys.argv[1])) if 'pdht' in r['Name']]" "$d/run_kernel_stats.csv" ;;
+    hyg_*)   cfg=${step#hyg_}; d="gpurun_out/hyg/$cfg"; mkdir -p "$d"
+             # one bench line and the rocprof kernel trace + stats OF THAT RUN (cfg2 without the
+             # configs[4] block, which has its own step: hyg_config4)
+             extra=""; [ "$cfg" = cfg2 ] && extra="--no-config4"
+             timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$d" -o run --output-format csv -- python3 bench.py --config $cfg $extra ${HYGARGS:-} > "$d/bench.json" 2> "$d/bench.err"; rc=$?
+             tail -1 "$d/bench.json" | cut -c1-300 ;;
     pmc_*)   cfg=${step#pmc_}; rc=0; i=0
              # PMCS: counter groups separated by ';' (one rocprofv3 pass each)
              IFS=';' read -ra groups <<< "${PMCS:-FETCH_SIZE;WRITE_SIZE}"
              for grp in "${groups[@]}"; do
                i=$((i+1))
-               timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_${cfg}_$i" -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/pmc_${cfg}_$i.log 2>&1 || { rc=$?; break; }
+               timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_${cfg}_$i" -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-host --no-config4 > gpurun_out/pmc_${cfg}_$i.log 2>&1 || { rc=$?; break; }
              done ;;
     sq_*)    cfg=${step#sq_}
              timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/sq_$cfg" -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-host > gpurun_out/sq_$cfg.log 2>&1; rc=$?
