@@ -50,7 +50,7 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
     // 8 keys per lane in flight (late r04, HBM-resident keys: 0.621 -> 0.681
     // against 4; 16: 0.629; profiles/r04/ab/ab_placerot_shapes.log)
     if (sink.hist && keylen == 8) {
-      g_kernel = "k_fixed_direct<8,8,nt,1024>@1";
+      g_kernel = PDHT_PLACE8_NT ? "k_fixed_direct<8,8,nt,1024>@1" : "k_fixed_direct<8,8,nt-store,1024>@1";
       k_fixed_direct<8, 8, Algo, SinkNt, PDHT_PLACE8_NT, 1024>
           <<<grid_for((blocks + 31) / 32, 1, dev), 1024, 0, st>>>(k, n, algo, snt);
       return;
