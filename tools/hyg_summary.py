@@ -6,10 +6,11 @@ tools/gpu_session.sh hyg_<cfg>).  For each config it prints
   * the bench line's own figures: Gkeys/s, roofline frac (algorithmic bytes
     over the HIP-event time per step), read-only GB/s;
   * the same frac recomputed from the trace: algorithmic bytes per step over
-    the summed kernel time per step of the step's launches -- the hash
-    kernel's dispatches of the timed steps (the K steps are the last K x
-    launches-per-step dispatches before the parity leg; warm-up and
-    calibration launches excluded);
+    the summed kernel time per step of the step's launches -- the step
+    kernels' dispatches of the K timed steps (the first K x launches-per-step
+    of them after the bench's Infinity-Cache flush; warm-up, calibration and
+    parity launches excluded), and the first-start-to-last-end span of those
+    dispatches per step (kernel time plus the gaps between launches);
   * their ratio, so a reader can check that the event timing and the kernel
     durations agree.
 
@@ -38,52 +39,55 @@ def load_line(path):
     return None
 
 
+LAUNCH_BYTES = 512 << 20  # launch.h kLaunchBytes
+
+
+def launches_per_step(line):
+    """Launches of the hash kernel per bench step (launch.h: fixed keys in
+    ~512-MiB launches of whole 4096-key blocks, k_global batches in one,
+    variable keys by the batch's mean key length)."""
+    c = line["config"]
+    n, kern = c["keys_per_gpu"], c["kernel"]
+    if kern.startswith("k_global"):
+        return 1
+    if kern.startswith("k_window<var"):
+        mean = max(1, int(c["bytes_per_key"] - 16))
+        if n * mean <= LAUNCH_BYTES:
+            return 1
+        step = max(4096, (LAUNCH_BYTES // mean) & ~4095)
+        return -(-n // step)
+    L = c["key_bytes"]
+    per = max(1, LAUNCH_BYTES // L)
+    if n <= per:
+        return 1
+    step = (per + 4095) & ~4095
+    return -(-n // step)
+
+
 def step_kernel_us(cfg, trace, line):
-    """Mean kernel microseconds per timed step, from the trace."""
+    """Mean kernel microseconds per timed step, from the trace: the timed
+    steps are the first K x launches-per-step dispatches of the step's
+    kernels after the Infinity-Cache flush (bench.py flush_infinity_cache,
+    a 512-MiB torch fill) that follows the warm-up."""
     rows = list(csv.DictReader(open(trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    steps, warm = line["steps"], line["warmup"]
+    steps = line["steps"]
     if cfg in STEP_KERNELS:
         pats = STEP_KERNELS[cfg]
-        sel = [r for r in rows if any(p in r["Kernel_Name"] for p in pats)]
-        base = [r for r in sel if "k_bucket_base" in r["Kernel_Name"]]  # one per bucketing
-        # the timed bucketings: the (warmup + 1)th .. (warmup + steps)th (the first
-        # bucketing of every rotation set is the set-up call before the warm-up)
-        starts = [int(r["Start_Timestamp"]) for r in base]
-        nsets = line["config"].get("rotation", {}).get("output_sets", 1)
-        first = nsets + warm
-        t0 = starts[first]
-        t1 = starts[first + steps] if first + steps < len(starts) else float("inf")
-        # a bucketing's count kernel starts before its base kernel: take the
-        # dispatches from the count kernel that precedes the first timed base
-        prev = [int(r["Start_Timestamp"]) for r in sel if int(r["Start_Timestamp"]) < t0
-                and ("count" in r["Kernel_Name"])]
-        lo = prev[-1] if prev else t0
-        prev1 = [int(r["Start_Timestamp"]) for r in sel if int(r["Start_Timestamp"]) < t1
-                 and ("count" in r["Kernel_Name"])]
-        hi = prev1[-1] if t1 != float("inf") and prev1 else t1
-        tim = [r for r in sel if lo <= int(r["Start_Timestamp"]) < hi]
-        tot = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tim)
-        return tot / 1e3 / steps, len(tim)
-    tag = line["config"]["kernel"]
-    head = tag.split("<")[0]
-    sel = [r for r in rows if head in r["Kernel_Name"]]
-    per = max(1, round(len(sel) / max(1, steps + warm + 1)))  # launches per step (512-MiB launches)
-    # the timed steps: after the warm-up, before anything else runs
-    idx = [i for i, r in enumerate(rows) if head in r["Kernel_Name"]]
-    # locate the K-step block: the longest run of consecutive same-kernel dispatches
-    runs, cur = [], [idx[0]]
-    for a, b in zip(idx, idx[1:]):
-        if b == a + 1:
-            cur.append(b)
-        else:
-            runs.append(cur)
-            cur = [b]
-    runs.append(cur)
-    block = max(runs, key=len)
-    timed = block[-steps * per:] if len(block) >= steps * per else block
-    tot = sum(int(rows[i]["End_Timestamp"]) - int(rows[i]["Start_Timestamp"]) for i in timed)
-    return tot / 1e3 / (len(timed) / per), len(timed)
+        is_step = lambda nm: any(p in nm for p in pats)  # noqa: E731
+        per = len(pats)
+    else:
+        head = line["config"]["kernel"].split("<")[0]
+        is_step = lambda nm: head in nm  # noqa: E731
+        per = launches_per_step(line)
+    first = next(i for i, r in enumerate(rows) if is_step(r["Kernel_Name"]))
+    flush = next(i for i, r in enumerate(rows) if i > first and "vectorized_elementwise_kernel<16" in r["Kernel_Name"])
+    timed = [r for r in rows[flush + 1:] if is_step(r["Kernel_Name"])][:steps * per]
+    if len(timed) != steps * per:
+        raise SystemExit(f"{cfg}: {len(timed)} timed dispatches, want {steps * per}")
+    tot = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed)
+    span = int(timed[-1]["End_Timestamp"]) - int(timed[0]["Start_Timestamp"])
+    return tot / 1e3 / steps, len(timed), span / 1e3 / steps
 
 
 def main():
@@ -102,10 +106,11 @@ def main():
         n = line["config"]["keys_per_gpu"]
         bpk = line["config"]["bytes_per_key"]
         ev_ms = line["roofline"]["event_ms_per_step"]
-        kus, nk = step_kernel_us(cfg, tr, line)
+        kus, nk, span_us = step_kernel_us(cfg, tr, line)
         frac_tr = bpk * n / (kus * 1e-6) / 1e9 / 8000.0
         row = {"cfg": cfg, "Gkeys_s": line["value"], "frac_event": line["roofline"]["frac"],
                "event_ms_per_step": ev_ms, "trace_ms_per_step": round(kus / 1e3, 4), "trace_dispatches": nk,
+               "trace_span_ms_per_step": round(span_us / 1e3, 4),
                "frac_trace": round(frac_tr, 4), "event_over_trace": round(ev_ms / (kus / 1e3), 4),
                "read_only_GBps": line["roofline"].get("read_only_GBps"), "kernel": line["config"]["kernel"],
                "parity": line["parity"].split(":")[0], "traffic": line["roofline"].get("traffic"),
