@@ -121,11 +121,13 @@ def main():
                "cpu": (line.get("cpu_baseline") or {}).get("value")}
         out.append(row)
     if md:
-        print("| cfg | kernel | Gkeys/s | frac (event) | frac (trace, same run) | event / trace | parity | CPU ref Gkeys/s |")
+        print("| config | kernel (tag) | Gkeys/s | frac, HIP events | frac, rocprof trace of the same run | "
+              "read-only frac | parity | CPU reference Gkeys/s |")
         print("|---|---|---|---|---|---|---|---|")
         for r in out:
+            ro = round(r["read_only_GBps"] / 8000.0, 4) if r["read_only_GBps"] else None
             print(f"| {r['cfg']} | `{r['kernel']}` | {r['Gkeys_s']} | {r['frac_event']} | {r['frac_trace']} | "
-                  f"{r['event_over_trace']} | {r['parity']} | {r['cpu']} |")
+                  f"{ro} | {r['parity']} | {r['cpu']} |")
     else:
         for r in out:
             print(json.dumps(r))
