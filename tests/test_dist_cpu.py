@@ -1,5 +1,7 @@
 """The N > 1 path on CPU: world_size-2 gloo processes run bench.py's sharding
-and reductions (pdht_amd.dist) over a small key stream.
+and reductions (pdht_amd.dist) over a small key stream -- and the same code in
+a gloo group of ONE process (what `bench.py --dist-backend` does at N = 1:
+the collectives and the exchange still run, every bucket to rank 0).
 
 Each rank hashes its weak-scaling shard with the product's scalar CityHash64
 (the same city_core.h code the kernels run), folds it by global key index and
@@ -19,7 +21,6 @@ import torch.multiprocessing as mp
 from conftest import ROOT
 
 N_PER = 3000
-WORLD = 2
 
 
 def _free_port():
@@ -96,7 +97,8 @@ def test_shard_helpers_single_process():
     assert D.fold_tensor(big, 0) == (1 << 64) - 1
 
 
-def test_two_rank_gloo_shards_and_reductions(oracle):
+@pytest.mark.parametrize("WORLD", [2, 1])
+def test_gloo_shards_and_reductions(oracle, WORLD):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -115,7 +117,7 @@ def test_two_rank_gloo_shards_and_reductions(oracle):
         assert r["local"] == r["oracle_local"]          # each shard checks on its own
         assert r["total"] == want_total                 # and they add up to the whole
         assert r["max"] == [float(WORLD), 0.5 * (WORLD - 1)]
-        assert r["ok_all"] is False                     # one failing rank fails all
+        assert r["ok_all"] is (WORLD == 1)              # one failing rank (rank 1) fails all
         pr = r["per_rank"]                              # every rank sees every rank's numbers
         assert pr["world_size"] == WORLD and pr["backend"] == "gloo"
         assert [x["rank"] for x in pr["ranks"]] == list(range(WORLD))
