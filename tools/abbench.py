@@ -129,6 +129,20 @@ def workload(name, dev):
             P.place_batch(ks[turn[0] % 4], 3, 1024, hist=hist, out=outs)
             turn[0] += 1
         return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * (L + 16)
+    if name.startswith("bucket8kn_"):
+        # bucket8krot's setup at n = <M> x 2^20 keys (per-key cost against n:
+        # how much of the two-pass intermediate the Infinity Cache holds)
+        n = int(name.split("_")[1]) * M
+        kk = [P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8) for _ in range(4)]
+        ws = torch.empty(P.bucket_workspace_bytes(n, 8, 8192), dtype=torch.uint8, device=dev)
+        sets = [P.bucket_batch(k, 3, 8192, workspace=ws) for k in kk]
+        turn = [0]
+
+        def step():
+            j = turn[0] % 4
+            turn[0] += 1
+            P.bucket_batch(kk[j], 3, 8192, out=sets[j], workspace=ws)
+        return step, (lambda: torch.cat([sets[0][1], sets[0][3].long(), sets[0][4]])), n * 32
     if name in ("bucketrot", "recordsrot", "bucket8krot"):
         # bucket / records at 1024 ranks (bucket8k: 8192 ranks, two passes)
         # with the keys rotated over 4 copies and the outputs over 4 sets, as
