@@ -787,8 +787,9 @@ constexpr u32 kTpMaxDigits = 256;
 constexpr u32 kTpChunkTiles = PDHT_TP_CHUNK_TILES;  // counting tiles per count-chunk (one count workgroup)
 struct TwoPass {
   u32 fbits, F, C, cbits;
-  const u32 *countsF;   // [ntiles][F] fine-bucket keys of tile t before it in its 32-tile chunk
-  const u32 *chunksF;   // [ntiles/32][F] ... of the 32-tile chunks before it
+  const u32 *countsF;   // [ntiles][F] fine-bucket keys of tile t before it in its fchunk-tile chunk
+  const u32 *chunksF;   // [ntiles/fchunk][F] ... of the chunks before it
+  u32 fchunk;           // tiles per fine-count chunk
   const u64 *totalsF;   // [F] keys per fine bucket
   const u32 *chunkcnt;  // [nchunks][nranks] keys of rank r in the count-chunks before chunk g
   const u64 *base;      // [nranks] first final slot of bucket r
@@ -799,7 +800,7 @@ struct TwoPass {
   u64 SG, nsegf, nseg;  // count-chunks per segment; segments per f; segments
   // keys of fine bucket f in the tiles before tile t (t <= ntiles)
   __device__ __forceinline__ u32 fine_before(u64 t, u32 f) const {
-    return t < ntiles ? countsF[t * F + f] + chunksF[(t / kBucketChunk) * F + f] : (u32)totalsF[f];
+    return t < ntiles ? countsF[t * F + f] + chunksF[(t / fchunk) * F + f] : (u32)totalsF[f];
   }
 };
 
@@ -809,10 +810,14 @@ struct TwoPass {
 // pass's per-tile rank rows are as large as the keys at high rank counts
 // (4096 tiles x 8192 ranks x 4 B = 128 MB for 16M keys, written, scanned and
 // read again); these are nranks/F and kTpChunkTiles times smaller.
+// With chunksF (fchunk = kTpChunkTiles), countsF[t][f] is already the
+// exclusive scan down the chunk and chunksF[g][f] the chunk's sum, so no
+// column scan of countsF follows.
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__restrict__ keys, u64 n, FastMod rk,
                                                             u32 nranks, u32 F, u32 *__restrict__ countsF,
-                                                            u32 *__restrict__ chunkcnt, u64 ntiles) {
+                                                            u32 *__restrict__ chunkcnt, u64 ntiles,
+                                                            u32 *__restrict__ chunksF) {
   constexpr int U = 128 / L;
   extern __shared__ u32 hist[];  // [nranks]
   __shared__ u32 fh[kTpMaxDigits];
@@ -820,6 +825,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__res
   const u64 nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
   for (u64 g = blockIdx.x; g < nchunks; g += gridDim.x) {
     for (u32 r = threadIdx.x; r < nranks; r += kBlock) hist[r] = 0;
+    u32 facc = 0;  // thread f < F: fine-f keys of the chunk's tiles so far
     const u64 t1 = min((g + 1) * kTpChunkTiles, ntiles);
     for (u64 t = g * kTpChunkTiles; t < t1; ++t) {
       if (threadIdx.x < F) fh[threadIdx.x] = 0;
@@ -839,8 +845,13 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__res
           }
       }
       __syncthreads();
-      if (threadIdx.x < F) countsF[t * F + threadIdx.x] = fh[threadIdx.x];
+      if (threadIdx.x < F) {
+        const u32 c = fh[threadIdx.x];
+        countsF[t * F + threadIdx.x] = chunksF ? facc : c;
+        facc += c;
+      }
     }
+    if (chunksF && threadIdx.x < F) chunksF[g * F + threadIdx.x] = facc;
     __syncthreads();
     for (u32 r = threadIdx.x; r < nranks; r += kBlock) chunkcnt[g * nranks + r] = hist[r];
     __syncthreads();
@@ -967,12 +978,19 @@ void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass
   }
 }
 
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8>
+// ONE (8-B keys into arrays, the default there since late r05): the sub-tile
+// stages {key, index} instead of {digest, index} and hashes each key a
+// second time in the store phase, so all four outputs of a key leave in one
+// phase -- two barriers and one LDS round per sub-tile fewer than staging the
+// digest first and the key bytes after it (staged_store).  Interleaved, 16M
+// keys at 8192 ranks: -1.0 to -1.3 % (profiles/r05/ab/bucket8k_pass2_one_store_phase.log).
+template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, bool ONE = (L == 8 && !Out::kPair8)>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
+  static_assert(!ONE || (L == 8 && !Out::kPair8), "one store phase: 8-B keys into arrays");
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
   extern __shared__ u64 lds64[];
-  u64 *stage = lds64;                                    // [kTile] digests, then key pieces
+  u64 *stage = lds64;                                    // [kTile] digests, then key pieces (ONE: keys)
   u32 *sidx = reinterpret_cast<u32 *>(stage + kTile);  // [kTile] original index
   __shared__ u32 runt[W * kTpMaxDigits];
   __shared__ u32 running[kTpMaxDigits];  // next final slot of bucket c*F + f
@@ -1012,12 +1030,13 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
         load_key_regs<L, true>(tp.ikeys, p, kr[g]);
         ix[g] = __builtin_nontemporal_load(tp.iidx + p);
       }
-      u64 h[KPL];
+      u64 h[ONE ? 1 : KPL];
       u32 cc[KPL];
 #pragma unroll
       for (int g = 0; g < KPL; ++g) {
-        h[g] = city64(kr[g], (u64)L);
-        cc[g] = coarse(h[g], 0u);
+        const u64 hh = city64(kr[g], (u64)L);
+        if constexpr (!ONE) h[g] = hh;
+        cc[g] = coarse(hh, 0u);
       }
       __syncthreads();
 #pragma unroll
@@ -1031,11 +1050,32 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
 #pragma unroll
       for (int g = 0; g < KPL; ++g)
         if (q0 + g * 64 < tn) {
-          stage[lp[g]] = h[g];
+          if constexpr (ONE)
+            stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
+          else
+            stage[lp[g]] = h[g];
           sidx[lp[g]] = ix[g];
         }
       __syncthreads();
-      staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
+      if constexpr (ONE) {
+        // thread j: staged key j -> hash again -> its slot; every output at once
+#pragma unroll
+        for (int jj = 0; jj < KPL; ++jj) {
+          const u32 j = jj * kB + threadIdx.x;
+          if (j < tn) {
+            RegReader<2> r;
+            const u64 key = stage[j];
+            r.d[0] = (u32)key;
+            r.d[1] = (u32)(key >> 32);
+            const u64 hv = city64(r, (u64)L);
+            const u32 slot = delta[coarse(hv, 0u)] + j;
+            out.meta(slot, hv, sidx[j]);
+            if (out.has_keys()) out.key8(slot, 0, key);
+          }
+        }
+      } else {
+        staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
+      }
       __syncthreads();
       if (threadIdx.x < tp.C) running[threadIdx.x] += tcount[threadIdx.x];
     }

@@ -55,12 +55,11 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
 #endif
   if (two_pass) {
     const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
-    const u64 tp_chunks32 = (tp_tiles + kBucketChunk - 1) / kBucketChunk;
     const u64 tp_chunks = (tp_tiles + kTpChunkTiles - 1) / kTpChunkTiles;
     w.countsF = reinterpret_cast<u32 *>(p + off);
     off += round256((size_t)tp_tiles * kTpMaxDigits * 4);
-    w.chunksF = reinterpret_cast<u32 *>(p + off);
-    off += round256((size_t)tp_chunks32 * kTpMaxDigits * 4);
+    w.chunksF = reinterpret_cast<u32 *>(p + off);  // rows of kTpChunkTiles (or kBucketChunk) tiles
+    off += round256((size_t)tp_chunks * kTpMaxDigits * 4);
     w.totalsF = reinterpret_cast<u64 *>(p + off);
     off += round256((size_t)kTpMaxDigits * 8);
     w.chunkcnt = reinterpret_cast<u32 *>(p + off);
@@ -137,14 +136,14 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
 // their units in the static XCD-contiguous order (TileOrder; per-XCD tickets
 // gained nothing here, r02 tuning variant 86).
 template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int W1 = W, int KPL1 = KPL,
-          int PER_CU1 = PER_CU>
+          int PER_CU1 = PER_CU, bool ONE = (L == 8 && !Out::kPair8)>
 static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
   constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;      // waves per SIMD, pass 2
   constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;  // pass 1
   const size_t b1 = pass1_lds_bytes<W1, KPL1>(), b2 = pass2_lds_bytes<W, KPL>();
   auto f1 = &k_bucket_pass1<L, W1, KPL1, WPE1>;
-  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE>;
+  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, ONE>;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
   const u64 cus = (u64)std::max(1, g_dev[dev].cus);
@@ -168,12 +167,21 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
   // long, half the barriers per key): 8-B keys at 8192 / 2048 ranks -11 /
   // -10.5 %, 32-B at 4096 -4 %; 16-B keys gain most with pass 2 in 8 x 8 @ 2
   // as well (-9 % at 4096 ranks; 8-B keys +4 % with it).  Pass 2 in 8 x 8 @ 3
-  // or 16 x 4 @ 2, pass 1 in 4 x 16 / 16 x 4 / 8 x 4: slower.
+  // or 16 x 4 @ 2, pass 1 in 4 x 16 / 16 x 4 / 8 x 4: slower.  Late r05:
+  // 8-B keys into arrays store from one phase (k_bucket_pass2 ONE) and take
+  // pass 2 in 8 x 8 @ 2 as well (4 x 8 @ 4 with ONE: equal to the two-phase
+  // product; 8 x 8 @ 2: -1.0 to -1.3 %, profiles/r05/ab/bucket8k_*.log).
 #ifdef PDHT_HIP_TUNING
   // (r04's shape search, tuning 192-201, removed in r05)
-  if (tuning_variant() == 202) return launch_two_pass<L, Out>(a, tp, out, st, dev);  // r02-r03: 4 x 8 @ 4 both
+  constexpr int kW = L == 8 && !Out::kPair8 ? 1 : 0;  // (ONE exists for 8-B arrays only)
+  if (tuning_variant() == 202)  // r02-r03: 4 x 8 @ 4 both, pass 2 storing in two phases
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, kTpW, kTpKPL, kTpPerCu, false>(a, tp, out, st, dev);
+  if (kW && tuning_variant() == 265)  // r04-r05 product for 8-B arrays: pass 2 two-phase 4 x 8 @ 4
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2, false>(a, tp, out, st, dev);
+  if (kW && tuning_variant() == 266)  // ONE in 4 x 8 @ 4
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
 #endif
-  if constexpr (L == 16)
+  if constexpr (L == 16 || (L == 8 && !Out::kPair8))
     return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
   else
     return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
@@ -304,22 +312,31 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     tp.nseg = (u64)tp.F * tp.nsegf;
   }
   if (ntiles && kind == BucketKernel::kTwoPass) {
-    const u64 nchunks32 = (ntiles + kBucketChunk - 1) / kBucketChunk;
+    // the count kernel scans the fine counts down each count-chunk itself
+    // (no column-scan launch); tuning 264: the r02-r05 colscan over 32-tile chunks
+    bool fscan = true;
+#ifdef PDHT_HIP_TUNING
+    if (tuning_variant() == 264) fscan = false;
+#endif
+    tp.fchunk = fscan ? kTpChunkTiles : kBucketChunk;
+    const u64 nfchunks = (ntiles + tp.fchunk - 1) / tp.fchunk;
+    u32 *cF = fscan ? w.chunksF : nullptr;
     const unsigned gc = (unsigned)std::min<u64>(tp.nchunks, (u64)std::max(1, g_dev[dev].cus) * 8);
     if (keysize == 8)
       k_bucket_count_tp<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                          ntiles);
+                                                          ntiles, cF);
     else if (keysize == 16)
       k_bucket_count_tp<16><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                           ntiles);
+                                                           ntiles, cF);
     else
       k_bucket_count_tp<32><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                           ntiles);
-    k_bucket_colscan<<<dim3((tp.F + 63) / 64, (unsigned)nchunks32), 64, 0, st>>>(w.countsF, ntiles, tp.F,
+                                                           ntiles, cF);
+    if (!fscan)
+      k_bucket_colscan<<<dim3((tp.F + 63) / 64, (unsigned)nfchunks), 64, 0, st>>>(w.countsF, ntiles, tp.F,
                                                                                    w.chunksF);
     const u32 nbF = (tp.F + 63) / 64;  // both chunk scans in one launch
     k_bucket_chunkscan2<<<nbF + (nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(
-        w.chunksF, nchunks32, tp.F, w.totalsF, nbF, w.chunkcnt, tp.nchunks, nranks, w.totals);
+        w.chunksF, nfchunks, tp.F, w.totalsF, nbF, w.chunkcnt, tp.nchunks, nranks, w.totals);
   } else if (ntiles) {
     const unsigned gc = grid_for(ntiles, 8, dev);
     if (fixed && keysize == 8)

@@ -557,6 +557,12 @@ BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
 # 202: the r03 two-pass sub-tile shape (4 x 8 @ 4 for both passes)
 BUCKET_CASES += [(L, nr, n, v) for v in (202,) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
+# 265 / 266: 8-B arrays' pass 2 as r04-r05 shipped it (two store phases, 4 x 8 @ 4) / one phase in 4 x 8 @ 4
+BUCKET_CASES += [(8, nr, n, v) for v in (265, 266) for nr in (1536, 2049, 8192)
+                 for n in (4095, 300007, (1 << 20) + 5)]
+# 264: the fine counts column-scanned over 32-tile chunks by k_bucket_colscan (r02-r05)
+BUCKET_CASES += [(L, nr, n, 264) for L in (8, 16, 32) for nr in (1536, 2049, 8192)
+                 for n in (4095, 300007, (1 << 20) + 5, (3 << 20) + 7)]
 # 164: two-pass arrays on the balanced digit split (the product takes one fine bit more)
 BUCKET_CASES += [(L, nr, n, 164) for L in (8, 16, 32) for nr in (1025, 2049, 4097, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
