@@ -120,8 +120,8 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * ptindex_out is best NULL.  nranks <= 8192, n < 2^32.  `workspace`
  * (device) must hold pdht_bucket_workspace_bytes(n, keysize, nranks): the
  * per-tile counts and, for 8/16/32-B keys at the rank counts that take the
- * two-pass sort (from 1536 / 1025 / 2049 ranks for 8 / 16 / 32-B keys), its
- * intermediate (n x (keysize + 4) bytes). */
+ * two-pass sort (from 1536 / 1025 / 1025 ranks for 8 / 16 / 32-B keys; 32-B
+ * arrays take it from 2049), its intermediate (n x (keysize + 4) bytes). */
 size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint32_t nptes, uint32_t nranks, void *workspace,

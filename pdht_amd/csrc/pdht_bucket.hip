@@ -23,8 +23,19 @@ static bool two_pass_keysize(size_t keysize) { return keysize == 8 || keysize ==
 // Two-pass bucketing from this many ranks up (interleaved
 // A/B on 16M keys; at 1024 ranks one pass is 10 % faster for 8-B keys, equal
 // for 16-B keys, 30 % faster for 32-B keys; at 2048 ranks two passes are 1.3x
-// faster for 8-B keys and at 8192 ranks 2.1x).
-static u32 two_pass_min_ranks(size_t keysize) { return keysize == 8 ? 1536 : keysize == 16 ? 1025 : 2049; }
+// faster for 8-B keys and at 8192 ranks 2.1x).  Late r05, with the 32-B
+// passes no longer spilling: 32-B records take two passes from 1025 ranks
+// (1024 ranks -3 %, 2048 ranks -13 %), 32-B arrays still from 2049 (one
+// pass 0.82 / 0.95 ms against two 0.95 / 0.99 at 1024 / 2048 ranks,
+// profiles/r05/ab/bucket_16_32_two_pass_shapes.log).
+static u32 two_pass_min_ranks(size_t keysize, bool records) {
+  return keysize == 8 ? 1536 : keysize == 16 ? 1025 : records ? 1025 : 2049;
+}
+// the workspace (sized without knowing the output kind) reserves the
+// intermediate from the lower of the two thresholds
+static u32 two_pass_reserve_ranks(size_t keysize) {
+  return std::min(two_pass_min_ranks(keysize, false), two_pass_min_ranks(keysize, true));
+}
 // Sized for the smallest tile any scatter kernel uses, plus the two-pass
 // intermediate when the batch can take that path: 8/16/32-B keys from
 // two_pass_min_ranks() up (the tuning build forces two passes at any nranks
@@ -51,7 +62,7 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
 #ifdef PDHT_HIP_TUNING
   const bool two_pass = two_pass_keysize(keysize);
 #else
-  const bool two_pass = two_pass_keysize(keysize) && nranks >= two_pass_min_ranks(keysize);
+  const bool two_pass = two_pass_keysize(keysize) && nranks >= two_pass_reserve_ranks(keysize);
 #endif
   if (two_pass) {
     const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
@@ -180,11 +191,38 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
     return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2, false>(a, tp, out, st, dev);
   if (kW && tuning_variant() == 266)  // ONE in 4 x 8 @ 4
     return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+  if constexpr (L >= 16) {  // r05 spill probe (16/32-B keys in 4 keys per lane) and the r04-r05 shapes
+    switch (tuning_variant()) {
+      case 267: return launch_two_pass<L, Out, 8, 4, 2, 8, 4, 2>(a, tp, out, st, dev);
+      case 268: return launch_two_pass<L, Out, 4, 4, 4, 8, 4, 2>(a, tp, out, st, dev);
+      case 269: return launch_two_pass<L, Out, 8, 4, 2, 4, 8, 4>(a, tp, out, st, dev);
+      case 270:
+        if constexpr (L == 16) return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
+        else return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+      default: break;
+    }
+  }
+  if constexpr (L == 8 && Out::kPair8) {  // 8-B records' pass 2: 4 x 4 @ 4 / r04-r05's 4 x 8 @ 4
+    if (tuning_variant() == 271) return launch_two_pass<L, Out, 4, 4, 4, 8, 8, 2>(a, tp, out, st, dev);
+    if (tuning_variant() == 272) return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+  }
 #endif
-  if constexpr (L == 16 || (L == 8 && !Out::kPair8))
+  // Late r05: at 8 keys per lane the 16/32-B kernels spilled VGPRs (pass 1
+  // of 32-B keys 78 registers, pass 2 58); in 4 keys per lane none spill
+  // (profiles/r05/ab/bucket_16_32_two_pass_shapes.log, 16M keys): 32-B arrays
+  // at 4096 / 8192 ranks 1.293 -> 0.936 / 1.327 -> 0.978 ms (both passes 8 x 4
+  // @ 2), 32-B records at 8192 ranks 1.728 -> 1.165 and 16-B records at 4096
+  // 0.751 -> 0.656 (pass 2 in 4 x 4 @ 4); 16-B arrays keep 8 x 8 @ 2 (4 keys
+  // per lane +5 %).  8-B records' pass 2 (5 VGPRs spilled at 4 x 8 @ 4) in 8 x
+  // 4 @ 2: 8192 / 2048 ranks 0.389 -> 0.369 / 0.363 -> 0.346 ms.
+  if constexpr (L == 32 && !Out::kPair8)
+    return launch_two_pass<L, Out, 8, 4, 2, 8, 4, 2>(a, tp, out, st, dev);
+  else if constexpr (L >= 16 && Out::kPair8)
+    return launch_two_pass<L, Out, 4, 4, 4, 8, 4, 2>(a, tp, out, st, dev);
+  else if constexpr (L == 16 || (L == 8 && !Out::kPair8))
     return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
   else
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+    return launch_two_pass<L, Out, 8, 4, 2, 8, 8, 2>(a, tp, out, st, dev);
 }
 
 enum class BucketKernel { kStaged, kGeneric, kTwoPass };
@@ -231,7 +269,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   // (two_pass_min_ranks <= kStagedMaxRanks + 1: the staged scatter covers
   // every nranks below the two-pass threshold)
   BucketKernel kind = !fixed                                ? BucketKernel::kGeneric
-                      : nranks >= two_pass_min_ranks(keysize) ? BucketKernel::kTwoPass
+                      : nranks >= two_pass_min_ranks(keysize, Out::kPair8) ? BucketKernel::kTwoPass
                                                               : BucketKernel::kStaged;
 #ifdef PDHT_HIP_TUNING
   // 21: the generic-length kernel for 8/16/32-B keys too; 70: one pass (the

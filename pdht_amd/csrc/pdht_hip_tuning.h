@@ -61,11 +61,19 @@ extern "C" {
  *                 71  two passes from 2 ranks up
  *              83/87  owner-table ranking on 8 x 16 / 4 x 16 tiles, any nranks
  *              85/89  ballot ranking, any nranks (85: static tile order)
- *                202  the r02-r03 two-pass sub-tile shape (4 x 8 @ 4 for both passes;
- *                     product since r04: pass 1 8x8@2, pass 2 4x8@4 (16-B keys 8x8@2));
- *                     r04's other shapes (192-201) and r05's LDS-DMA pipelined passes,
- *                     packed pass-1 tables and prefetching count kernel (230-242) were
+ *                202  the r02-r03 two-pass sub-tile shape (4 x 8 @ 4 for both passes,
+ *                     pass 2 storing in two phases); r04's other shapes (192-201), r05's
+ *                     LDS-DMA pipelined passes, packed pass-1 tables and prefetching
+ *                     count kernel (230-242) and higher-occupancy shapes (253-259) were
  *                     measured slower and removed
+ *                264  fine counts column-scanned over 32-tile chunks (k_bucket_colscan,
+ *                     r02-r05; product: the count kernel scans down its own chunk)
+ *            265/266  8-B arrays' pass 2 as r04-r05 shipped it (two store phases, 4x8@4) /
+ *                     one store phase in 4x8@4 (product: one phase, 8x8@2)
+ *            267-269  16/32-B keys' two passes: 8x4@2 both / pass 2 4x4@4 / pass 1 4x8@4,
+ *                     pass 2 8x4@2 (product: 32-B arrays 267, 16/32-B records 268)
+ *                270  16/32-B keys' two passes as r04-r05 shipped them (spilling)
+ *            271/272  8-B records' pass 2 in 4x4@4 / 4x8@4 (r04-r05; product 8x4@2)
  *                164  two-pass arrays of 8/16-B keys on the balanced digit split
  *                     F = 2^ceil(nbits/2) (product: one fine bit more)
  *   records      112  r02 store order (header halves a staging round early)

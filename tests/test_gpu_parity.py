@@ -563,6 +563,9 @@ BUCKET_CASES += [(8, nr, n, v) for v in (265, 266) for nr in (1536, 2049, 8192)
 # 264: the fine counts column-scanned over 32-tile chunks by k_bucket_colscan (r02-r05)
 BUCKET_CASES += [(L, nr, n, 264) for L in (8, 16, 32) for nr in (1536, 2049, 8192)
                  for n in (4095, 300007, (1 << 20) + 5, (3 << 20) + 7)]
+# 267-269: 16/32-B keys' two passes in 4 keys per lane (r05 spill probe)
+BUCKET_CASES += [(L, nr, n, v) for v in (267, 268, 269, 270) for L in (16, 32) for nr in (2049, 8192)
+                 for n in (4095, 300007, (1 << 20) + 5)]
 # 164: two-pass arrays on the balanced digit split (the product takes one fine bit more)
 BUCKET_CASES += [(L, nr, n, 164) for L in (8, 16, 32) for nr in (1025, 2049, 4097, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
@@ -582,7 +585,7 @@ def _bucket_kernel(L, nranks, variant, records=False):
     if variant == 21:
         return wg
     if L in (8, 16, 32):
-        two_pass_from = {8: 1536, 16: 1025, 32: 2049}[L]
+        two_pass_from = {8: 1536, 16: 1025, 32: 1025 if records else 2049}[L]
         one_pass = variant == 70 and nranks <= 2048
         if (variant == 71 and nranks >= 2) or (not one_pass and nranks >= two_pass_from):
             return f"k_bucket_pass2<{L}B>"
@@ -678,6 +681,12 @@ RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n i
 # records switch to owner-table ranking for 16/32-B keys from 512 ranks while
 # two workgroups fit a CU (staged_shape): both edges of both thresholds
 RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]
+# 32-B records take two passes from 1025 ranks (arrays from 2049)
+RECORD_CASES += [(32, nr, n, 0) for nr in (1024, 1025, 2048) for n in (4097, 300007)]
+# two-pass shapes of records: 267-270 (16/32-B keys), 271 / 272 (8-B keys' pass 2 in 4 keys per lane)
+RECORD_CASES += [(L, nr, n, v) for v in (267, 268, 269, 270) for L in (16, 32) for nr in (2049, 8192)
+                 for n in (4097, 300007)]
+RECORD_CASES += [(8, nr, n, v) for v in (271, 272) for nr in (2049, 8192) for n in (4097, 300007, (1 << 20) + 5)]
 # 112: the r02 store order of 8-B records (header halves a staging round early)
 RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
 

@@ -231,7 +231,7 @@ def test_bucket_workspace_small_at_low_rank_counts():
     """The two-pass intermediate (n x (keysize + 4) B) is reserved only at
     the rank counts that take the two-pass sort."""
     n = 16 << 20
-    for L, thr in ((8, 1536), (16, 1025), (32, 2049)):
+    for L, thr in ((8, 1536), (16, 1025), (32, 1025)):  # 32-B: records' threshold (arrays: 2049)
         small = P.bucket_workspace_bytes(n, L, 1024 if L != 16 else 1000)
         assert small < 64 << 20, (L, small)
         assert P.bucket_workspace_bytes(n, L, thr) >= small + n * (L + 4)
@@ -267,6 +267,8 @@ def test_every_tuning_variant_is_documented():
                   if not p.endswith("pdht_hip_tuning.h"))
     used = {int(x) for x in re.findall(r"tuning_variant\(\) == (\d+)", src)}
     used |= {int(x) for x in re.findall(r"\bv == (\d+)", src)}
+    for block in re.findall(r"switch \(tuning_variant\(\)\) \{(.*?)\n\s*\}", src, re.S):
+        used |= {int(x) for x in re.findall(r"case (\d+):", block)}
     for lo, hi in re.findall(r"v >= (\d+) && v <= (\d+)", src):
         used |= set(range(int(lo), int(hi) + 1))
     doc = open(os.path.join(ROOT, "pdht_amd", "csrc", "pdht_hip_tuning.h")).read()
