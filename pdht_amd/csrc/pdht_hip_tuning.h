@@ -64,7 +64,8 @@ extern "C" {
  *                202  the r02-r03 two-pass sub-tile shape (4 x 8 @ 4 for both passes,
  *                     pass 2 storing in two phases); r04's other shapes (192-201), r05's
  *                     LDS-DMA pipelined passes, packed pass-1 tables and prefetching
- *                     count kernel (230-242) and higher-occupancy shapes (253-259) were
+ *                     count kernel (230-242), higher-occupancy shapes (253-259) and 8-B
+ *                     arrays in 4 keys per lane (273-276) were
  *                     measured slower and removed
  *                264  fine counts column-scanned over 32-tile chunks (k_bucket_colscan,
  *                     r02-r05; product: the count kernel scans down its own chunk)
