@@ -236,13 +236,27 @@ struct AlgoCrc128Seed {
 // 6-bit form's 11 of ~3.  Byte-indexed tables conflict in LDS (+72 % bank
 // conflicts), but the long-key loop is VALU-heavy and the byte tables run
 // 3-4 % faster (interleaved, `profiles/r03/ab/long_bytetab_*.log`).
+// Late r05: the eight lookups are folded with gfx950's three-input v_bitop3
+// (XOR3) -- 4 VALU instead of 7 per word; the long-key loop spends most of
+// its VALU on these folds (PDHT_CRC_XOR3=0: the plain xor chain, A/B only).
+#ifndef PDHT_CRC_XOR3
+#define PDHT_CRC_XOR3 1
+#endif
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) {
+#if PDHT_CRC_XOR3
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // truth table of a ^ b ^ c
+#else
+  return a ^ b ^ c;
+#endif
+}
 struct CrcLdsByteTab {
   const u32 *t;  // [8][256], table k for byte k of the word (= slice-8 table 7-k)
   __device__ __forceinline__ u32 rd(u32 k, u32 b) const { return t[256 * k + b]; }
   __device__ __forceinline__ u32 crc64(u64 x) const {
     const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    return rd(0, lo & 255) ^ rd(1, (lo >> 8) & 255) ^ rd(2, (lo >> 16) & 255) ^ rd(3, lo >> 24) ^
-           rd(4, hi & 255) ^ rd(5, (hi >> 8) & 255) ^ rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24);
+    const u32 a = xor3(rd(0, lo & 255), rd(1, (lo >> 8) & 255), rd(2, (lo >> 16) & 255));
+    const u32 b = xor3(rd(3, lo >> 24), rd(4, hi & 255), rd(5, (hi >> 8) & 255));
+    return xor3(a, b, rd(6, (hi >> 16) & 255) ^ rd(7, hi >> 24));
   }
 };
 

@@ -427,4 +427,197 @@ __global__ __launch_bounds__(kBlock) void k_window_wc(const uint8_t *__restrict_
   }
 }
 
+
+// ------------------------------------------- long keys through an LDS ring ---
+// r05 experiment (tuning 279-282): fixed keys of L = 1024 / 2048 / 4096 B on
+// the CityHashCrc256 path.  The product walks each lane's key with per-lane
+// loads (every wave instruction touches 64 lines).  Here the wave's 64 keys
+// stream through a ring of R line-rounds in LDS (a round = one 128-B line of
+// each of the 64 keys, 8 KiB), filled by COALESCED LDS-DMA: in DMA
+// instruction i, lanes 8j..8j+7 fetch the 8 pieces of key 8i+j's line, in an
+// order rotated by i + j so that the per-lane reads that follow are free of
+// bank conflicts (piece p of key k = 8i+j sits at slot ((p - i - j) & 7)).
+// The hash runs Crc256Stream (line-by-line), reading each line from the ring
+// into registers; the moment a line is read its slot takes the line R ahead
+// (the next tile's first lines at the end of a tile), so R - 1 rounds are
+// always in flight and no VGPR holds them.  Waits are exact: when line l is
+// read, the lines issued after it are l+1 .. l+R-1 (8 DMA instructions
+// each; a digest store in between only makes the wait stricter); the last
+// tile waits for everything.
+__device__ __forceinline__ void lds_dma16(const void *g, u32 lds) {
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  u32 save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_c() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int L, int R>
+struct LongRing {
+  static constexpr int NL = L / 128;                                  // lines per key
+  static constexpr int kBlocks = L / 240;
+  static constexpr int kStreamLines = (240 * kBlocks + 127) / 128;  // lines the block loop streams
+  static constexpr int kLate = kStreamLines - 1;                     // first line kept for the tail
+  static_assert(L % 128 == 0 && L > 900, "whole lines, CityHashCrc256 path");
+  static_assert(R >= NL - kStreamLines + 1 && R <= NL && R * 8 <= 63, "ring depth");
+  static constexpr int kTailWait = 8 * (R + kStreamLines - NL - 1);
+};
+
+// A wave's view of its ring (every member wave-uniform except the lane's own
+// offsets).  line_lim() reads line l of the lane's key and hands the slot to
+// the line R ahead; span() serves the tail chunks from the late lines.
+template <int L, int R>
+struct RingReader {
+  typedef LongRing<L, R> G;
+  static constexpr bool kStream = true;
+  uint8_t *ring;        // this wave's R slots of 8 KiB (LDS)
+  u32 ring_lds;         // the same, as an LDS byte address (DMA base)
+  u32 kofs, rot;        // lane's key row inside a slot; its piece rotation
+  u32 seq0;             // ring sequence number of this tile's line 0
+  const uint8_t *cur;   // keys of this tile's DMA rows (lane-specific, clamped), line 0
+  const uint8_t *nxt;   // the next tile's (nullptr: this is the wave's last tile)
+  u32 dma_rot;          // lane's DMA piece rotation base: (lane & 7) + (lane >> 3)
+  u64 dma_step;         // bytes from DMA instruction i's row to i+1's (8 keys)
+  u64 last_row_off;     // clamp: offset of the batch's last row from `cur` / `nxt` (per tile)
+  u64 nxt_last_row_off;
+
+  __device__ __forceinline__ u32 slot(u32 l) const { return ((seq0 + l) % R) * 8192u; }
+  __device__ __forceinline__ void wait_line(u32 l) const {
+    if (nxt == nullptr)
+      vm_wait_c<0>();
+    else
+      vm_wait_c<8 * (R - 1)>();
+  }
+  // DMA line l of the tile whose rows start at base (lane-specific) into slot s
+  __device__ __forceinline__ void issue(const uint8_t *base, u64 last_off, u32 l, u32 s) const {
+#pragma unroll
+    for (u32 i = 0; i < 8; ++i) {
+      const u64 off = min((u64)i * dma_step, last_off);
+      const u32 p = (dma_rot + i) & 7;
+      lds_dma16(base + off + 128u * l + 16u * p, ring_lds + s + i * 1024u);
+    }
+  }
+  // the slot of line l is free: fetch the line R ahead into it
+  __device__ __forceinline__ void release(u32 l) const {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads have landed
+    const u32 ahead = l + R;
+    if (ahead < (u32)G::NL)
+      issue(cur, last_row_off, ahead, slot(l));
+    else if (nxt)
+      issue(nxt, nxt_last_row_off, ahead - G::NL, slot(l));
+  }
+  __device__ __forceinline__ const uint8_t *at(u32 o) const {  // byte o of the lane's key (resident line)
+    const u32 l = o >> 7, p = (o >> 4) & 7;
+    return ring + slot(l) + kofs + ((p - rot) & 7) * 16 + (o & 15);
+  }
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> line_lim(u32 o, u32) const {
+    static_assert(N == 128, "whole lines");
+    const u32 l = o >> 7;
+    wait_line(l);
+    Words<32> w;
+    typedef u32 u32x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (u32 p = 0; p < 8; ++p) {
+      const u32x4v v = *reinterpret_cast<const u32x4v *>(ring + slot(l) + kofs + ((p - rot) & 7) * 16);
+      w.d[4 * p] = v.x;
+      w.d[4 * p + 1] = v.y;
+      w.d[4 * p + 2] = v.z;
+      w.d[4 * p + 3] = v.w;
+    }
+    if (l < (u32)G::kLate) release(l);
+    return w;
+  }
+  template <int N>
+  __device__ __forceinline__ Words<N / 4> span(u32 o) const {
+    Words<N / 4> w;
+    if ((o + N - 1) >> 7 > (u32)G::kLate) {  // a line only the tail reads: its DMA
+      if (nxt == nullptr)
+        vm_wait_c<0>();
+      else
+        vm_wait_c<G::kTailWait>();
+    }
+    if ((o & 7) == 0 && N % 8 == 0) {
+#pragma unroll
+      for (int j = 0; j < N / 8; ++j) {
+        const u64 v = *reinterpret_cast<const u64 *>(at(o + 8 * j));
+        w.d[2 * j] = (u32)v;
+        w.d[2 * j + 1] = (u32)(v >> 32);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < N / 4; ++j) w.d[j] = w32(o + 4 * j);
+    }
+    return w;
+  }
+  __device__ __forceinline__ u32 b8(u32 o) const { return *at(o); }
+  __device__ __forceinline__ u32 w32(u32 o) const {
+    return b8(o) | (b8(o + 1) << 8) | (b8(o + 2) << 16) | (b8(o + 3) << 24);
+  }
+};
+
+template <int L, int R, class Algo, class Sink>
+__global__ __launch_bounds__(256) void k_long_ring(const uint8_t *__restrict__ keys, u64 n, Algo algo, Sink sink) {
+  typedef LongRing<L, R> G;
+  extern __shared__ __attribute__((aligned(16))) uint8_t ring_all[];  // [4 waves][R][8 KiB]
+  __shared__ u32 lds_hist[Sink::kHist];
+  sink.lds_hist = lds_hist;
+  algo_init(algo);
+  sink.init();
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const u64 ntiles = (n + 63) / 64, nwaves = (u64)gridDim.x * 4;
+  u64 t = (u64)blockIdx.x * 4 + wave;
+  if (t < ntiles) {
+    RingReader<L, R> rd;
+    rd.ring = ring_all + wave * (R * 8192);
+    rd.ring_lds = (u32)(uintptr_t)rd.ring;
+    rd.kofs = (lane >> 3) * 1024 + (lane & 7) * 128;
+    rd.rot = (lane >> 3) + (lane & 7);
+    rd.dma_rot = (lane & 7) + (lane >> 3);
+    rd.dma_step = 8ull * L;
+    // DMA rows of tile tt for this lane: key 64 tt + 8 i + (lane >> 3) in instruction i
+    auto rows = [&](u64 tt, u64 &last_off) {
+      const u64 first = tt * 64 + (lane >> 3);
+      last_off = (n - 1 >= first ? n - 1 - first : 0) * (u64)L;  // rows past the batch re-read its last key
+      return keys + min(first, n - 1) * (u64)L;
+    };
+    rd.seq0 = 0;
+    rd.cur = rows(t, rd.last_row_off);
+    u64 tn = t + nwaves;
+    rd.nxt = tn < ntiles ? rows(tn, rd.nxt_last_row_off) : nullptr;
+    // the first tile's first R lines
+#pragma unroll
+    for (u32 l = 0; l < (u32)R; ++l) rd.issue(rd.cur, rd.last_row_off, l, l * 8192u);
+    while (true) {
+      const u64 i = t * 64 + lane;
+      const auto h = algo(rd, (u64)L);
+      // the tail has read the late lines: their slots take the lines R ahead
+      if (rd.nxt == nullptr)
+        vm_wait_c<0>();
+#pragma unroll
+      for (u32 l = G::kLate; l < (u32)G::NL; ++l) rd.release(l);
+      if (i < n) sink.put(i, h);
+      if (rd.nxt == nullptr) break;
+      t = tn;
+      tn = t + nwaves;
+      rd.seq0 += G::NL;
+      rd.cur = rd.nxt;
+      rd.last_row_off = rd.nxt_last_row_off;
+      rd.nxt = tn < ntiles ? rows(tn, rd.nxt_last_row_off) : nullptr;
+    }
+  }
+  sink.flush();
+}
+
 }  // namespace pdht

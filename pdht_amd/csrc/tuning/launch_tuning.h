@@ -166,6 +166,28 @@ template <class Algo, class Sink>
 static int tuning_crc_long(const uint8_t *k, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
                            hipStream_t st, int dev, u64 blocks) {
   const int v = tuning_variant();
+  if (v >= 279 && v <= 281 && stride == keylen && (keylen == 1024 || keylen == 2048 || keylen == 4096)) {
+    // the LDS-DMA ring (k_long_ring): R = 4 / 2 / 3 line-rounds per wave
+    typedef typename NtSink<Sink>::type SinkNt;
+    const SinkNt sink_nt = NtSink<Sink>::make(sink);
+    const int R = v == 279 ? 4 : v == 280 ? 2 : 3;
+    const int per_cu = R == 2 ? 2 : 1;
+    const size_t lds = (size_t)4 * R * 8192;
+    const unsigned g = (unsigned)std::min<u64>((n + 255) / 256, (u64)std::max(1, g_dev[dev].cus) * per_cu);
+    auto go = [&](auto kern, const char *tag) {
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      g_kernel = tag;
+      kern<<<g, 256, lds, st>>>(k, n, algo, sink_nt);
+      return tuning_launched();
+    };
+#define PDHT_RING(LL, RR) \
+  if (keylen == LL && R == RR) return go(&k_long_ring<LL, RR, Algo, SinkNt>, "k_long_ring<" #LL "," #RR ">");
+    PDHT_RING(1024, 4) PDHT_RING(1024, 2) PDHT_RING(1024, 3)
+    PDHT_RING(2048, 4) PDHT_RING(2048, 2) PDHT_RING(2048, 3)
+    PDHT_RING(4096, 4) PDHT_RING(4096, 2) PDHT_RING(4096, 3)
+#undef PDHT_RING
+  }
   if (v != 190 && v != 191) return kNoVariant;
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt sink_nt = NtSink<Sink>::make(sink);

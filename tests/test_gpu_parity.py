@@ -167,6 +167,28 @@ def test_crc128_long_keys_line_stream(dev, oracle, L, variant):
     assert [tuple(int(x) for x in g) for g in gs] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:200]]
 
 
+@pytest.mark.tuning
+@pytest.mark.parametrize("variant", [279, 280, 281])
+@pytest.mark.parametrize("L,n", [(1024, 1), (1024, 63), (1024, 64), (1024, 3001), (1024, 70_001),
+                                 (2048, 3001), (2048, 20_033), (4096, 5000)])
+def test_crc128_long_keys_lds_ring(dev, oracle, L, n, variant):
+    """Tuning variants 279-281: packed long keys through an LDS-DMA ring of
+    coalesced line-rounds (k_long_ring): single keys, one exact tile, ragged
+    tiles, several tiles per wave (70 001 keys) and the key at the very end of
+    its allocation; seeded variant too."""
+    rng = np.random.default_rng(L + n + variant)
+    k = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    kd = to_dev(k, dev)
+    with P.tuning(variant):
+        got = u64(P.citycrc128_batch(kd))
+        kern = P.last_kernel()
+        s0, s1 = 0x0123456789ABCDEF, 0xFEDCBA9876543210
+        gs = u64(P.citycrc128_seed_batch(kd[:200], (s0, s1))).reshape(-1, 2)
+    assert kern.startswith("k_long_ring<"), kern
+    assert (got == oracle.city128_fixed(k, crc=True)).all()
+    assert [tuple(int(x) for x in g) for g in gs] == [oracle.citycrc128_seed(r.tobytes(), s0, s1) for r in k[:200]]
+
+
 @pytest.mark.parametrize("L", [0, 5, 8, 16, 24, 32, 64, 100, 256, 300, 384, 400, 1200])
 def test_seeded_batches(dev, oracle, L):
     rng = np.random.default_rng(77 + L)
