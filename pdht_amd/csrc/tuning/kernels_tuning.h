@@ -44,14 +44,13 @@ struct LdsReaderFunnel {
 // indices stay conflict-free, at 11 lookups per word against 8.
 struct CrcLds6Tab {
   const u32 *t;  // [11][64]
-  __device__ __forceinline__ u32 crc64(u64 x) const {
+  __device__ __forceinline__ u32 crc64(u64 x) const {  // (late r05: XOR3 folds, as the byte tables)
     const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    u32 r = t[0 * 64 + (lo & 63)] ^ t[1 * 64 + ((lo >> 6) & 63)] ^ t[2 * 64 + ((lo >> 12) & 63)] ^
-            t[3 * 64 + ((lo >> 18) & 63)] ^ t[4 * 64 + ((lo >> 24) & 63)];
-    r ^= t[5 * 64 + (__builtin_amdgcn_alignbit(hi, lo, 30) & 63)];
-    r ^= t[6 * 64 + ((hi >> 4) & 63)] ^ t[7 * 64 + ((hi >> 10) & 63)] ^ t[8 * 64 + ((hi >> 16) & 63)] ^
-         t[9 * 64 + ((hi >> 22) & 63)] ^ t[10 * 64 + (hi >> 28)];
-    return r;
+    const u32 a = xor3(t[0 * 64 + (lo & 63)], t[1 * 64 + ((lo >> 6) & 63)], t[2 * 64 + ((lo >> 12) & 63)]);
+    const u32 b = xor3(t[3 * 64 + ((lo >> 18) & 63)], t[4 * 64 + ((lo >> 24) & 63)],
+                       t[5 * 64 + (__builtin_amdgcn_alignbit(hi, lo, 30) & 63)]);
+    const u32 c = xor3(t[6 * 64 + ((hi >> 4) & 63)], t[7 * 64 + ((hi >> 10) & 63)], t[8 * 64 + ((hi >> 16) & 63)]);
+    return xor3(xor3(a, b, c), t[9 * 64 + ((hi >> 22) & 63)], t[10 * 64 + (hi >> 28)]);
   }
 };
 
