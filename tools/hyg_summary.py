@@ -31,8 +31,9 @@ STEP_KERNELS = {
                  "k_bucket_scatter"],
     "xrecords": ["k_bucket_count_reg", "k_bucket_colscan", "k_bucket_chunkscan", "k_bucket_base",
                  "k_bucket_scatter"],
-    "bucket8k": ["k_bucket_count_tp", "k_bucket_colscan", "k_bucket_chunkscan2", "k_bucket_base",
-                 "k_bucket_pass1", "k_bucket_pass2"],
+    # (late r05: the two-pass count kernel scans its fine counts itself, no colscan launch)
+    "bucket8k": ["k_bucket_count_tp", "k_bucket_chunkscan2", "k_bucket_base", "k_bucket_pass1",
+                 "k_bucket_pass2"],
 }
 
 
