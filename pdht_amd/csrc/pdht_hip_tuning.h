@@ -23,6 +23,7 @@ extern "C" {
  *                206  s_setprio 1 around each wave's prefetch issue
  *              80/81  1024-thread transpose at 1 / 2 WG/CU (cfg1 shape)
  *                 82  the 256-thread transpose whatever the histogram
+ *            250/251  tile order scattered (bijection) / per-wave contiguous runs
  *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
  *                153  timing only: CRC lookups replaced by a fold (wrong digests)
  *                150  CRC-32C on r02's 6-bit-slice tables (product: byte tables)
@@ -31,6 +32,7 @@ extern "C" {
  *            190/191  CityHashCrc256Long's block loop as a 128-B line stream
  *                     (kLongStream), 8 / 4 WG/CU
  *   var keys      12  10224-B window at 4 WG/CU;  13 16 KiB window at 2 WG/CU
+ *                252  workgroup-combined digest stores (4 consecutive tiles, 2 KiB runs)
  *            170-173  CityHash64: k_window_pipe (offsets a tile ahead, digests a tile
  *                     late, vmcnt(2)): G = 1 / 4 / 16 consecutive tiles per wave at
  *                     4 WG/CU; 173 = G 1 at 3 WG/CU; 174 = G 1 / 175 = the product

@@ -263,7 +263,8 @@ def test_every_tuning_variant_is_documented():
     pdht_hip_tuning.h (the list had gone stale)."""
     import glob
     import re
-    src = "".join(open(p).read() for p in glob.glob(os.path.join(ROOT, "pdht_amd", "csrc", "*.h*"))
+    src = "".join(open(p).read() for p in glob.glob(os.path.join(ROOT, "pdht_amd", "csrc", "*.h*")) +
+                  glob.glob(os.path.join(ROOT, "pdht_amd", "csrc", "tuning", "*.h"))
                   if not p.endswith("pdht_hip_tuning.h"))
     used = {int(x) for x in re.findall(r"tuning_variant\(\) == (\d+)", src)}
     used |= {int(x) for x in re.findall(r"\bv == (\d+)", src)}
