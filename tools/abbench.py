@@ -129,6 +129,36 @@ def workload(name, dev):
             P.place_batch(ks[turn[0] % 4], 3, 1024, hist=hist, out=outs)
             turn[0] += 1
         return step, (lambda: torch.cat([outs[0], outs[1].long(), outs[2].long()])), n * (L + 16)
+    if name in ("bucket2s", "bucket8k2s", "records2s"):
+        # two batches per step, bucketed concurrently on two streams (each its
+        # own workspace and outputs; keys and outputs rotated over 4 sets):
+        # the bulk-loader shape of consecutive batches in flight together
+        n = 16 * M
+        nr = 8192 if name == "bucket8k2s" else 1024
+        kk = [P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8) for _ in range(4)]
+        wss = [torch.empty(P.bucket_workspace_bytes(n, 8, nr), dtype=torch.uint8, device=dev) for _ in range(2)]
+        rec = name == "records2s"
+        sets = [P.bucket_records(k, nr, workspace=wss[0]) if rec else P.bucket_batch(k, 3, nr, workspace=wss[0])
+                for k in kk]
+        strs = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        turn = [0]
+
+        def step():
+            cur = torch.cuda.current_stream(dev)
+            for s_ in strs:
+                s_.wait_stream(cur)
+            for q in range(2):
+                j = (turn[0] + q) % 4
+                with torch.cuda.stream(strs[q]):
+                    if rec:
+                        P.bucket_records(kk[j], nr, out=sets[j], workspace=wss[q], stream=strs[q])
+                    else:
+                        P.bucket_batch(kk[j], 3, nr, out=sets[j], workspace=wss[q], stream=strs[q])
+            turn[0] += 2
+            for s_ in strs:
+                cur.wait_stream(s_)
+        per = 40 if rec else 32
+        return step, (lambda: sets[0][1][:1 << 20].clone()), 2 * n * per
     if name.startswith("bucket8kn_"):
         # bucket8krot's setup at n = <M> x 2^20 keys (per-key cost against n:
         # how much of the two-pass intermediate the Infinity Cache holds)
