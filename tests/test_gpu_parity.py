@@ -1117,6 +1117,33 @@ def test_chunked_launches(dev, oracle, variant):
     assert (dv == oracle.city64_var(dh, oh)).all()
 
 
+def test_more_than_4G_keys(dev, oracle):
+    """Batches of more than 2^32 keys (8-B keys: 32 GiB in, 32 GiB of
+    digests, then the fused placement with a histogram): every index past
+    2^31 and 2^32 lands where it belongs -- checked against the oracle on
+    samples around both boundaries and at the ends, the histogram against
+    the batch size and the rank array."""
+    n = (1 << 32) + 4099
+    kd = P.splitmix64_fill(0x4A11, 0, n, device=dev).view(torch.uint8).view(n, 8)
+    idx = np.unique(np.concatenate([np.arange(0, 100), np.arange((1 << 31) - 100, (1 << 31) + 100),
+                                    np.arange((1 << 32) - 100, (1 << 32) + 100), np.arange(n - 100, n)]))
+    kh = kd[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    d64 = P.city64_batch(kd)
+    assert (u64(d64[torch.from_numpy(idx).to(dev)]) == oracle.city64_fixed(kh)).all()
+    del d64
+    torch.cuda.empty_cache()
+    hist = torch.zeros(7, dtype=torch.int64, device=dev)
+    mb, pt, rk = P.place_batch(kd, 3, 7, hist=hist)
+    m2, p2, r2 = oracle.pdht_hash_fixed(kh, 3, 7)
+    ti = torch.from_numpy(idx).to(dev)
+    assert (u64(mb[ti]) == m2).all() and (pt[ti].cpu().numpy().view(np.uint32) == p2).all()
+    assert (rk[ti].cpu().numpy().view(np.uint32) == r2).all()
+    assert int(hist.sum().item()) == n
+    assert [int(hist[r].item()) for r in range(7)] == [int((rk == r).sum().item()) for r in range(7)]
+    del kd, mb, pt, rk
+    torch.cuda.empty_cache()
+
+
 def test_var_offsets_check_on_launch_stream(dev, oracle):
     """The variable-length wrappers' default offsets check reads offsets[0] /
     offsets[n] on the LAUNCH stream: offsets written on a side
