@@ -1144,6 +1144,33 @@ def test_more_than_4G_keys(dev, oracle):
     torch.cuda.empty_cache()
 
 
+def test_var_keys_past_4GiB(dev, oracle):
+    """Offset-indexed keys whose bytes run past 2^32 (36M mixed 16..256-B
+    keys, ~4.9 GB in several launches): the keys whose bytes straddle or lie
+    beyond the 2^31 / 2^32 byte offsets, and the last ones, against the
+    oracle."""
+    nv = 36 << 20
+    lens = P.mixed_lengths(0x1E575EED1E575EED, 0, nv, 16, 256, device=dev)
+    offs = torch.zeros(nv + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item())
+    assert total > (1 << 32) + (1 << 28)
+    data = P.splitmix64_fill(0x5EED, 0, (total + 7) // 8, device=dev).view(torch.uint8)[:total]
+    dv = P.city64_var_batch(data, offs)
+    oh = offs.cpu().numpy()
+    idx = []
+    for b in (1 << 31, 1 << 32):
+        j = int(np.searchsorted(oh, b, side="right")) - 1  # the key holding byte b
+        idx += list(range(j - 50, j + 50))
+    idx = np.unique(np.array(idx + list(range(nv - 100, nv))))
+    sub = [data[int(oh[i]):int(oh[i + 1])].cpu().numpy() for i in idx]
+    so = np.concatenate([[0], np.cumsum([len(x) for x in sub])]).astype(np.uint64)
+    want = oracle.city64_var(np.concatenate(sub), so)
+    assert (u64(dv[torch.from_numpy(idx).to(dev)]) == want).all()
+    del data, dv, offs, lens
+    torch.cuda.empty_cache()
+
+
 def test_var_offsets_check_on_launch_stream(dev, oracle):
     """The variable-length wrappers' default offsets check reads offsets[0] /
     offsets[n] on the LAUNCH stream: offsets written on a side
