@@ -1144,6 +1144,51 @@ def test_more_than_4G_keys(dev, oracle):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("nranks", [1000, 8192])
+def test_bucket_largest_batch(dev, oracle, nranks):
+    """Bucketing at the ABI's limit, n = 2^32 - 1 keys (32 GiB of 8-B keys;
+    the single pass at 1000 ranks, two passes at 8192): the per-rank counts
+    equal those of the fused placement over the input, every output key's
+    rank is its bucket's, indices rise strictly inside each bucket, each
+    output key is the input key its index names, and sampled digests match
+    the oracle -- together: the exact stable bucketing."""
+    n = (1 << 32) - 1
+    kd = P.splitmix64_fill(0xB16B, 0, n, device=dev).view(torch.uint8).view(n, 8)
+    hist = torch.zeros(nranks, dtype=torch.int64, device=dev)
+    P.place_batch(kd, 3, nranks, ptindex=False, rank=False, hist=hist)
+    torch.cuda.empty_cache()
+    ko, mb, pt, ix, offs = P.bucket_batch(kd, 3, nranks, with_ptindex=False)
+    torch.cuda.empty_cache()
+    assert int(offs[-1].item()) == n and int(offs[0].item()) == 0
+    assert (offs[1:] - offs[:-1] == hist).all()
+    step = 1 << 28
+    prev_r = prev_i = None
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        kc = ko[lo:hi]
+        _, _, rk = P.place_batch(kc, 3, nranks, ptindex=False)
+        rk = rk.long()
+        i64 = ix[lo:hi].long() & 0xFFFFFFFF
+        assert (rk[1:] >= rk[:-1]).all()  # buckets in rank order
+        same = rk[1:] == rk[:-1]
+        assert (i64[1:][same] > i64[:-1][same]).all()  # stable inside a bucket
+        if prev_r is not None and prev_r == int(rk[0].item()):
+            assert int(i64[0].item()) > prev_i
+        prev_r, prev_i = int(rk[-1].item()), int(i64[-1].item())
+        assert (kd[i64] == kc).all()  # the key its index names
+        del rk, i64, same
+    # the ranks' bucket bounds: the first key of every non-empty bucket has that rank
+    nz = torch.nonzero(hist).flatten()
+    starts = offs[nz]
+    _, _, rs = P.place_batch(ko[starts].contiguous(), 3, nranks, ptindex=False)
+    assert (rs.long() == nz).all()
+    sample = torch.from_numpy(np.unique(np.concatenate([np.arange(0, 64), np.arange(n - 64, n),
+                                                        np.random.default_rng(5).integers(0, n, 256)]))).to(dev)
+    assert (u64(mb[sample]) == oracle.city64_fixed(ko[sample].cpu().numpy())).all()
+    del kd, ko, mb, pt, ix, offs
+    torch.cuda.empty_cache()
+
+
 def test_var_keys_past_4GiB(dev, oracle):
     """Offset-indexed keys whose bytes run past 2^32 (36M mixed 16..256-B
     keys, ~4.9 GB in several launches): the keys whose bytes straddle or lie
