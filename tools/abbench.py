@@ -159,6 +159,23 @@ def workload(name, dev):
                 cur.wait_stream(s_)
         per = 40 if rec else 32
         return step, (lambda: sets[0][1][:1 << 20].clone()), 2 * n * per
+    if name.startswith("bucketn_"):
+        # bucketn_<M>_<nranks>: 8-B keys, n = M x 2^20, keys and outputs
+        # rotated over 4 sets (per-key cost against n at any rank count)
+        _, mm, nr = name.split("_")
+        n, nr = int(mm) * M, int(nr)
+        kk = [P.splitmix64_fill(SEED, 0, n, device=dev).view(torch.uint8).view(n, 8) for _ in range(4)]
+        with P.tuning(0):
+            wsb = P.bucket_workspace_bytes(n, 8, nr)
+        ws = torch.empty(max(wsb, P.bucket_workspace_bytes(n, 8, nr)), dtype=torch.uint8, device=dev)
+        sets = [P.bucket_batch(k, 3, nr, workspace=ws) for k in kk]
+        turn = [0]
+
+        def step():
+            j = turn[0] % 4
+            turn[0] += 1
+            P.bucket_batch(kk[j], 3, nr, out=sets[j], workspace=ws)
+        return step, (lambda: torch.cat([sets[0][1], sets[0][3].long(), sets[0][4]])), n * 32
     if name.startswith("bucket8kn_"):
         # bucket8krot's setup at n = <M> x 2^20 keys (per-key cost against n:
         # how much of the two-pass intermediate the Infinity Cache holds)
