@@ -192,7 +192,7 @@ __global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan(u32 *__restr
   chunkscan_block(blockIdx.x, chunks, nchunks, nranks, totals);
 }
 // Two independent chunk scans in one launch (two-pass bucketing: the fine
-// buckets' 32-tile chunk sums and the ranks' count-chunk histograms): blocks
+// buckets' count-chunk sums and the ranks' count-chunk histograms): blocks
 // [0, nb1) scan the first, the rest the second.
 __global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan2(u32 *__restrict__ c1, u64 n1, u32 w1,
                                                                      u64 *__restrict__ t1, u32 nb1,
@@ -760,12 +760,12 @@ void k_bucket_scatter_staged(
 //   pass 1 (k_bucket_pass1): per counting tile, the tile's keys in fine-bucket
 //          order into the intermediate at fbase[f] + (fine-f keys of earlier
 //          tiles), stable: the intermediate is ordered by (f, original index);
-//   pass 2 (k_bucket_pass2): per segment = (f, SG consecutive chunks of
-//          kBucketChunk tiles), a contiguous stretch of the intermediate that
+//   pass 2 (k_bucket_pass2): per segment = (f, SG consecutive count-chunks
+//          of kTpChunkTiles tiles), a contiguous stretch of the intermediate that
 //          holds, in original order, the fine-f keys of those tiles.  Sorted
 //          by c in sub-tiles of 4096 keys, each key goes to its final slot:
 //          bucket r = c * F + f receives the segment's keys at base[r] +
-//          chunks[g0][r] onwards, in order.
+//          chunkcnt[g0][r] onwards, in order.
 // Both passes take their positions from the single pass's per-tile counts
 // (count kernel + scans): no extra counting and no inter-workgroup waits.
 #ifndef PDHT_TP_TILE  // compile-time experiments only (make exp EXP=-DPDHT_TP_TILE=...)

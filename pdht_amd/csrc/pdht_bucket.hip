@@ -9,8 +9,9 @@ struct BucketWs {
   u32 *counts, *chunks;
   u64 *totals, *base, *fbase;
   u32 *tickets;  // [8] per-XCD tile tickets of the dynamic scatter
-  // two-pass sort (8/16/32-B keys): fine-bucket counts per tile and per
-  // 32-tile chunk, fine totals, rank counts per count-chunk, and the
+  // two-pass sort (8/16/32-B keys): fine-bucket counts per tile (scanned
+  // down each count-chunk) and per count-chunk, fine totals, rank counts per
+  // count-chunk, and the
   // intermediate ([n][keysize] key rows + [n] original indices)
   u32 *countsF, *chunksF, *chunkcnt;
   u64 *totalsF;
