@@ -775,10 +775,18 @@ void k_bucket_scatter_staged(
 #define PDHT_TP_CHUNK_TILES 8
 #endif
 #ifndef PDHT_TP_SEG_KEYS
-#define PDHT_TP_SEG_KEYS 4096
+#define PDHT_TP_SEG_KEYS 3840
 #endif
 constexpr u32 kTpCountTile = PDHT_TP_TILE;  // counting tile = pass-1 unit
-constexpr u32 kTpSegKeys = PDHT_TP_SEG_KEYS;  // pass-2 segment: ~this many keys of one fine bucket
+// Pass-2 segment: ~this many keys of one fine bucket.  A segment's length
+// is a sum of per-chunk counts (binomial): at a mean of 4096 keys (r02-r05)
+// half the segments held a few dozen keys more than one 4096-key sub-tile
+// and ran a second, nearly empty sub-tile through the whole phase chain.
+// 4096 - 4 sigma = 3840 keeps them in one (and in whole 2048 / 1024-key
+// sub-tiles): 8-B keys at 8192 / 2048 ranks -10.6 / -6.7 %, 16-B keys at
+// 4096 -4.5 %, 8-B records -1.6 %, 32-B keys within +-1.2 %
+// (profiles/r05/ab/bucket_pass2_segment_keys.log).
+constexpr u32 kTpSegKeys = PDHT_TP_SEG_KEYS;
 // F, C <= 256.  nranks <= 8192 = 2^13: the balanced split gives F = 2^7,
 // C = 2^6; the fine-plus split of 8/16-B array outputs (late r03,
 // pdht_bucket.hip) F = 2^8 -- at this bound -- and C = 2^5.  The launcher
