@@ -805,7 +805,7 @@ struct TwoPass {
   uint8_t *ikeys;       // [n][L] intermediate key rows
   u32 *iidx;            // [n] intermediate original indices
   u64 ntiles, nchunks;  // counting tiles; count-chunks of kTpChunkTiles tiles
-  u64 SG, nsegf, nseg;  // count-chunks per segment; segments per f; segments
+  u64 SG, nsegf, nseg;  // count-chunks per segment (about); segments per f; segments
   // keys of fine bucket f in the tiles before tile t (t <= ntiles)
   __device__ __forceinline__ u32 fine_before(u64 t, u32 f) const {
     return t < ntiles ? countsF[t * F + f] + chunksF[(t / fchunk) * F + f] : (u32)totalsF[f];
@@ -1013,8 +1013,8 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
   auto coarse = [&](u64 h, u32) { return (u32)rk.mod(h) >> fbits; };
   for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
     const u32 f = (u32)(o.t / tp.nsegf);
-    const u64 g0 = (o.t % tp.nsegf) * tp.SG;
-    const u64 g1 = min(g0 + tp.SG, tp.nchunks);
+    const u64 sg = o.t % tp.nsegf;  // the f-bucket's count-chunks split evenly over nsegf segments
+    const u64 g0 = sg * tp.nchunks / tp.nsegf, g1 = (sg + 1) * tp.nchunks / tp.nsegf;
     if (threadIdx.x == 0) {
       const u32 lo = tp.fine_before(g0 * kTpChunkTiles, f);
       seg[0] = lo;

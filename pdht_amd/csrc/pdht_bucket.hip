@@ -4,6 +4,9 @@
 #include "runtime.h"
 
 // ------------------------------------------------- destination bucketing ---
+#ifndef PDHT_TP_EVEN_SEG  // compile-time A/B only
+#define PDHT_TP_EVEN_SEG 1
+#endif
 namespace pdht {
 struct BucketWs {
   u32 *counts, *chunks;
@@ -347,7 +350,19 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     tp.ntiles = ntiles;
     tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
     tp.SG = std::max<u64>(1, (u64)tp.F * kTpSegKeys / ((u64)kTpChunkTiles * kTpCountTile));  // ~kTpSegKeys keys
-    tp.nsegf = (tp.nchunks + tp.SG - 1) / tp.SG;
+    // Segments per fine bucket: the count-chunks are split evenly.  When the
+    // remainder of nchunks / SG leaves at most one extra chunk per segment,
+    // take the floor (segments of SG or SG + 1 chunks: ~3968 keys at most,
+    // spilling ~2 % of the time) rather than the ceiling, whose segments
+    // are ~6 % shorter in the mean but one more per fine bucket -- one more
+    // pass through the sub-tile's phase chain (16M keys at 8192 ranks: 17
+    // segments of 30-31 chunks instead of 18).  Interleaved against the
+    // ceiling, both split evenly (profiles/r05/ab/bucket_pass2_even_segments.log):
+    // 8-B records at 8192 ranks -1.8 % (two 2048-key sub-tiles per segment
+    // either way, 34 sub-tiles per fine bucket instead of 36), arrays within
+    // +-0.5 %.  PDHT_TP_EVEN_SEG=0 (experiment builds): the ceiling.
+    const u64 nfl = std::max<u64>(1, tp.nchunks / tp.SG);
+    tp.nsegf = PDHT_TP_EVEN_SEG && tp.nchunks - nfl * tp.SG <= nfl ? nfl : (tp.nchunks + tp.SG - 1) / tp.SG;
     tp.nseg = (u64)tp.F * tp.nsegf;
   }
   if (ntiles && kind == BucketKernel::kTwoPass) {
