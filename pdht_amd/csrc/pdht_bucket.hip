@@ -361,8 +361,12 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     // 8-B records at 8192 ranks -1.8 % (two 2048-key sub-tiles per segment
     // either way, 34 sub-tiles per fine bucket instead of 36), arrays within
     // +-0.5 %.  PDHT_TP_EVEN_SEG=0 (experiment builds): the ceiling.
+    // (only where SG + 1 chunks stay ~2 sigma under 4096 keys: F = 256; at
+    // F <= 128 one chunk more is 256+ keys and would spill half the time)
     const u64 nfl = std::max<u64>(1, tp.nchunks / tp.SG);
-    tp.nsegf = PDHT_TP_EVEN_SEG && tp.nchunks - nfl * tp.SG <= nfl ? nfl : (tp.nchunks + tp.SG - 1) / tp.SG;
+    const u64 step = (u64)kTpChunkTiles * kTpCountTile / tp.F;  // keys of one fine bucket per chunk
+    const bool floor_ok = PDHT_TP_EVEN_SEG && (tp.SG + 1) * step <= 3968 && tp.nchunks - nfl * tp.SG <= nfl;
+    tp.nsegf = floor_ok ? nfl : (tp.nchunks + tp.SG - 1) / tp.SG;
     tp.nseg = (u64)tp.F * tp.nsegf;
   }
   if (ntiles && kind == BucketKernel::kTwoPass) {
