@@ -173,7 +173,8 @@ def plan(a, world: int) -> dict:
     `value` and, for the default config, the BASELINE configs[4] block -- the
     1B x 64 B stream split over the N ranks (strong scaling), timed beside
     the cfg2 weak-scaling value at every N."""
-    p = {"config": a.config, "value_scaling": "weak", "world_size": world, "backend": a.dist_backend}
+    p = {"config": a.config, "value_scaling": "strong" if a.config == "config4" else "weak",
+         "world_size": world, "backend": a.dist_backend}
     if a.config == "cfg2" and not a.no_config4 and not a.keys_per_gpu:
         p["config4"] = {"keys_total": CONFIG4_KEYS, "key_bytes": 64, "split": "strong (contiguous, 1B/N per rank)",
                         "keys_per_rank": [CONFIG4_KEYS * (r + 1) // world - CONFIG4_KEYS * r // world
@@ -226,6 +227,10 @@ def main():
             sys.exit(2)
     elif a.gpus is not None and a.gpus > 1:
         sys.exit(launch_ranks(a.gpus))  # before anything touches a GPU
+    if a.config == "config4" and a.keys_per_gpu:
+        sys.stderr.write("bench.py: --config config4 is BASELINE configs[4] (1B keys split over the ranks); "
+                         "--keys-per-gpu does not apply to it\n")
+        sys.exit(2)
     if a.dry_run:
         dry_run(a)
         return
@@ -589,12 +594,28 @@ def main():
     if world > 1 or dist.is_initialized():
         res["per_rank"] = D.per_rank_report(rank, local, world, n, bytes_per_key, kern_ms, elapsed, a.steps,
                                             PEAK_HBM_GBPS, device=dev)
-    if cfg in ("cfg2", "cfg4", "cfg5", "cfg1") and not a.no_host:  # (cfg2r: the same host path as cfg2)
-        hr = host_rate(P, torch, n, cfg, D, dev, cdev)
+    if cfg in ("cfg2", "cfg3", "cfg4", "cfg5", "cfg1") and not a.no_host:  # (cfg2r: the same host path as cfg2)
+        hr = host_rate(P, torch, n, cfg, D, dev, cdev, var=(data, offs, out) if cfg == "cfg3" else None)
         if rank == 0:
             res["host_resident"] = hr
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds, out, P, torch)
+    if not a.no_cpu_baseline:
+        # The reference city.c on this node's host cores, in the same run at
+        # every N: rank 0 alone, after every rank's GPU leg has finished and
+        # while the others sleep in a blocking (gloo) barrier, so no rank is
+        # hashing or spinning on a core meanwhile.  Keys 0.. of the stream are
+        # rank 0's shard at every N, so its GPU digests still check the sample.
+        cpu_wait = None
+        if world > 1:
+            cpu_wait = dist.new_group(backend="gloo") if backend == "nccl" else dist.group.WORLD
+            torch.cuda.synchronize()
+            dist.barrier(group=cpu_wait)
+        if rank == 0:
+            res["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds, out, P, torch)
+            if world > 1:
+                res["cpu_baseline"]["while"] = (f"rank 0 of {world}, after every rank's GPU leg; the other "
+                                                f"{world - 1} ranks blocked in a gloo barrier")
+        if cpu_wait is not None:
+            dist.barrier(group=cpu_wait)
     if "config4" in plan(a, world):
         del keys, out, words
         kset = rsets = bsets = calls = None  # noqa: F841 (free the rotation copies)
@@ -899,32 +920,65 @@ def check_records(P, torch, D, sh, keys, b, dev, cdev):
     return combine_parity(D, st, msgs, sh.world, cdev)
 
 
-def host_rate(P, torch, n, cfg, D, dev, cdev):
+def host_rate(P, torch, n, cfg, D, dev, cdev, var=None):
     """Host-resident rate: pinned keys in, pinned digests out, through the
     C-ABI host entry point (zero-copy for pinned buffers; PCIe-bound).  At
     N > 1 every rank runs at the same time on its own GPU (its own PCIe
-    link): per-rank rates and the aggregate over the slowest rank."""
+    link): per-rank rates and the aggregate over the slowest rank.
+
+    `var` = (bytes, offsets, digests) of cfg3's offset-indexed keys on the
+    device: the first 16M keys (4M at N > 1) are copied into pinned host
+    bytes + offsets, hashed through pdht_city64_batch_var_host, and the host
+    digests compared with the device run's digests of the same keys (which
+    the line's parity checks against the reference folds)."""
     import torch.distributed as dist
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
     try:
         m = min(n, 16 * M if world == 1 else 4 * M)
-        keys = torch.empty((m, 64), dtype=torch.uint8).pin_memory()
-        keys.view(-1).view(torch.int64).copy_(P.splitmix64_fill(SEED_KEYS, rank * m * 8, m * 8, device=dev).cpu())
-        w = 2 if cfg == "cfg4" else 1
-        out = torch.empty((m, w) if w == 2 else (m,), dtype=torch.int64).pin_memory()
-        fn = P.citycrc128_batch_host if cfg == "cfg4" else P.city64_batch_host
-        fn(keys, out=out, device=dev.index)  # warm-up
+        match = None
+        if var is not None:
+            vdata, voffs, vout = var
+            nb = int(voffs[m].item())
+            hdata = torch.empty(nb, dtype=torch.uint8).pin_memory()
+            hdata.copy_(vdata[:nb])
+            hoffs = torch.empty(m + 1, dtype=torch.int64).pin_memory()
+            hoffs.copy_(voffs[:m + 1])
+            out = torch.empty(m, dtype=torch.int64).pin_memory()
+            out.fill_(0)
+            bpk = nb / m + 8 + 8  # key bytes + offset + digest over PCIe
+
+            def fn():
+                P.city64_var_batch_host(hdata, hoffs, out=out, device=dev.index)
+            fn()  # warm-up
+            match = bool(torch.equal(out, vout[:m].cpu()))
+        else:
+            keys = torch.empty((m, 64), dtype=torch.uint8).pin_memory()
+            keys.view(-1).view(torch.int64).copy_(
+                P.splitmix64_fill(SEED_KEYS, rank * m * 8, m * 8, device=dev).cpu())
+            w = 2 if cfg == "cfg4" else 1
+            out = torch.empty((m, w) if w == 2 else (m,), dtype=torch.int64).pin_memory()
+            hfn = P.citycrc128_batch_host if cfg == "cfg4" else P.city64_batch_host
+            bpk = 64 + 8 * w
+
+            def fn():
+                hfn(keys, out=out, device=dev.index)
+            fn()  # warm-up
         reps = 3
         D.barrier()
         t0 = time.perf_counter()
         for _ in range(reps):
-            fn(keys, out=out, device=dev.index)
+            fn()
         dt = (time.perf_counter() - t0) / reps
         D.barrier()
-        mine = {"Gkeys_s": round(m / dt / 1e9, 4), "GBps_pcie": round(m * (64 + 8 * w) / dt / 1e9, 2)}
+        mine = {"Gkeys_s": round(m / dt / 1e9, 4), "GBps_pcie": round(m * bpk / dt / 1e9, 2), "match": match}
         res = {"value": mine["Gkeys_s"], "unit": "Gkeys/s", "keys": m, "GBps_pcie": mine["GBps_pcie"],
                "note": "pinned host keys and digests; the kernel reads/writes them over PCIe (zero-copy)"}
+        if var is not None:
+            res["note"] = ("pinned host key bytes + u64 offsets (the first keys of this rank's cfg3 stream) and "
+                           "pinned digests; the window kernel reads/writes them over PCIe (zero-copy)")
+            res["key_bytes"] = nb
+            res["digests_equal_device_run"] = match
         if world > 1:
             dtmax = D.allreduce_max([dt], device=cdev)[0]
             allr = [None] * world
@@ -934,6 +988,8 @@ def host_rate(P, torch, n, cfg, D, dev, cdev):
                        per_rank_GBps_pcie=[r["GBps_pcie"] for r in allr],
                        note=res["note"] + f"; {world} GPUs at once, one PCIe link each; value = all keys / "
                                           "slowest rank")
+            if var is not None:
+                res["digests_equal_device_run"] = all(r["match"] for r in allr)
         return res
     except Exception as e:  # pragma: no cover
         return {"error": str(e)}

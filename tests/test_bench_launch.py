@@ -81,6 +81,17 @@ def test_config4_block_only_on_default_workload():
     assert "config4" not in bench.plan(mk(keys_per_gpu=1000), 2)
 
 
+def test_config4_line_is_strong_scaling_and_rejects_keys_per_gpu():
+    sys.path.insert(0, ROOT)
+    import bench
+    a = type("A", (), {"config": "config4", "no_config4": False, "keys_per_gpu": 0, "dist_backend": None})
+    assert bench.plan(a, 8)["value_scaling"] == "strong"
+    p = subprocess.run([sys.executable, BENCH, "--config", "config4", "--keys-per-gpu", "1000", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=_env())
+    assert p.returncode == 2 and "--keys-per-gpu" in p.stderr
+    assert _json_lines(p.stdout) == []
+
+
 def test_gloo_rehearsal_flag_accepted():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-backend", "gloo", "--dry-run"],
                        capture_output=True, text=True, timeout=300, env=_env())

@@ -97,8 +97,10 @@ def test_shard_helpers_single_process():
     assert D.fold_tensor(big, 0) == (1 << 64) - 1
 
 
-@pytest.mark.parametrize("WORLD", [2, 1])
+@pytest.mark.parametrize("WORLD", [2, 1, 3, 8])
 def test_gloo_shards_and_reductions(oracle, WORLD):
+    """World sizes 1 and 2, a non-power-of-two 3, and 8 -- the driver's
+    scaling run -- so the exchange's 8-way splits are checked as well."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

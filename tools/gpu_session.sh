@@ -76,6 +76,10 @@ for step in "$@"; do
     rehearse4) # N = 4 the same way: 4 ranks on device 0 (configs[4] = 4 x 256M keys)
              timeout -k 10 800 python bench.py --gpus 4 --dist-backend gloo > gpurun_out/rehearse4.log 2>&1; rc=$?
              tail -1 gpurun_out/rehearse4.log | cut -c1-1500 ;;
+    rehearse8) # N = 8, the driver's scaling run, the same way: 8 ranks on device 0 (cfg2 shards 0..7,
+             # configs[4] = 8 x 128M keys, the CPU baseline on rank 0 while the others wait)
+             timeout -k 10 900 python bench.py --gpus 8 --dist-backend gloo > gpurun_out/rehearse8.log 2>&1; rc=$?
+             tail -1 gpurun_out/rehearse8.log | cut -c1-1500 ;;
     torchrun1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-host > gpurun_out/torchrun1.log 2>&1; rc=$?
              tail -1 gpurun_out/torchrun1.log | cut -c1-600 ;;
     *) echo "unknown step $step"; rc=0 ;;
