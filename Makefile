@@ -5,7 +5,8 @@
 #                      pdht_amd/lib/libpdht_hip_mpi.so (the same engine with
 #                      the libmpipdht flavour of pdht_hash, libmpipdht/hash.c)
 #                      pdht_amd/lib/libpdht_hip_tuning.so (tools/ and A/B
-#                      tests: alternative kernels, -DPDHT_HIP_TUNING)
+#                      tests: the same sources with the A/B hook headers of
+#                      pdht_amd/csrc/tuning/ instead of pdht_amd/csrc/product/)
 #                      oracle/liboracle.so, oracle/_ref/*.so (test checker)
 #   make product    -> only the product libraries
 #
@@ -22,17 +23,20 @@ LIB_MPI := $(LIBDIR)/libpdht_hip_mpi.so
 LIB_TUN := $(LIBDIR)/libpdht_hip_tuning.so
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden \
            -Wall -Wno-unused-function -munsafe-fp-atomics -Iinclude
+# "pdht_hooks*.h": the product's (every A/B hook a no-op) or the tuning build's
+HOOKS_PRODUCT := -Ipdht_amd/csrc/product
+HOOKS_TUNING  := -Ipdht_amd/csrc/tuning
 CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
 HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/runtime.h \
            pdht_amd/csrc/bucket.h pdht_amd/csrc/launch.h \
-           pdht_amd/csrc/tuning/kernels_tuning.h pdht_amd/csrc/tuning/launch_tuning.h \
+           $(wildcard pdht_amd/csrc/product/*.h) $(wildcard pdht_amd/csrc/tuning/*.h) \
            pdht_amd/csrc/pdht_hip_tuning.h include/pdht_hip.h include/pdht_city.h
 SHIM_HDR := include/pdht_hash.h include/pdht_hip.h include/pdht_city.h
 # the C-ABI in translation units that build in parallel (make -j)
 HIP_UNITS := pdht_hip pdht_fixed64 pdht_fixed128 pdht_var pdht_host pdht_bucket
 OBJ_ENG := $(HIP_UNITS:%=$(LIBDIR)/%.o) $(LIBDIR)/city_host.o
-OBJ_TUN_ENG := $(HIP_UNITS:%=$(LIBDIR)/%.tun.o) $(LIBDIR)/city_host.o
+OBJ_TUN_ENG := $(HIP_UNITS:%=$(LIBDIR)/%.tun.o) $(LIBDIR)/city_host.o $(LIBDIR)/pdht_tuning.tun.o
 OBJ     := $(OBJ_ENG) $(LIBDIR)/pdht_hash.o
 OBJ_MPI := $(OBJ_ENG) $(LIBDIR)/pdht_hash_mpi.o
 OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
@@ -43,7 +47,7 @@ OBJ_TUN := $(OBJ_TUN_ENG) $(LIBDIR)/pdht_hash.o
 EXP ?=
 EXP_TAG ?=
 LIB_EXP := $(LIBDIR)/libpdht_hip_exp$(if $(EXP_TAG),_$(EXP_TAG)).so
-OBJ_EXP := $(HIP_UNITS:%=$(LIBDIR)/%.exp.o) $(LIBDIR)/city_host.o $(LIBDIR)/pdht_hash.o
+OBJ_EXP := $(HIP_UNITS:%=$(LIBDIR)/%.exp.o) $(LIBDIR)/city_host.o $(LIBDIR)/pdht_tuning.tun.o $(LIBDIR)/pdht_hash.o
 
 .PHONY: all product oracle clean asm exp
 all: product oracle
@@ -56,15 +60,19 @@ $(foreach u,pdht_fixed64 pdht_fixed128 pdht_var pdht_host,$(LIBDIR)/$(u).o $(LIB
 
 $(LIBDIR)/%.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(HOOKS_PRODUCT) -c -o $@ $<
 
 $(LIBDIR)/%.tun.o: pdht_amd/csrc/%.hip $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DPDHT_HIP_TUNING -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(HOOKS_TUNING) -c -o $@ $<
+
+$(LIBDIR)/pdht_tuning.tun.o: pdht_amd/csrc/tuning/pdht_tuning.hip $(HIP_HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) $(HOOKS_TUNING) -c -o $@ $<
 
 $(LIBDIR)/%.exp.o: pdht_amd/csrc/%.hip $(HIP_HDR) FORCE
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DPDHT_HIP_TUNING $(EXP) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(HOOKS_TUNING) $(EXP) -c -o $@ $<
 
 exp: $(OBJ_EXP)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIB_EXP) $(OBJ_EXP)
@@ -94,7 +102,7 @@ oracle:
 # ISA listing of the kernels (for register / instruction counts)
 asm:
 	@mkdir -p build
-	for u in $(HIP_UNITS); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/$$u.s pdht_amd/csrc/$$u.hip || exit 1; done
+	for u in $(HIP_UNITS); do $(HIPCC) $(HIPFLAGS) $(HOOKS_PRODUCT) --cuda-device-only -S -o build/$$u.s pdht_amd/csrc/$$u.hip || exit 1; done
 
 clean:
 	rm -f $(LIBDIR)/*.o $(LIB) $(LIB_MPI) $(LIB_TUN) $(LIBDIR)/libpdht_hip_exp*.so

@@ -285,7 +285,7 @@ def main():
         words = P.splitmix64_fill(SEED_KEYS, sh.first * L // 8, n * L // 8, device=dev)
         keys = words.view(torch.uint8).view(n, L)
         nr = 1024 if cfg == "records" else world
-        ws = torch.empty(P.bucket_workspace_bytes(n, L, nr), dtype=torch.uint8, device=dev)
+        ws = torch.empty(P.bucket_workspace_bytes(n, L, nr, records=True), dtype=torch.uint8, device=dev)
         kset = rot_copies(torch, keys)
         rsets = [P.bucket_records(k, nr, src_rank=rank, workspace=ws) for k in kset]
         bucketed = {"nranks": nr, "records": True}

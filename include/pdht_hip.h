@@ -37,10 +37,13 @@ extern "C" {
 #define PDHT_HIP_OK 0
 #define PDHT_HIP_ERROR 1 /* == PdhtStatusError */
 /* ABI revision of this header; pdht_hip_version() names the same number
- * ("abi 3").  Revision 2 changed index_out to uint32_t, gave
+ * ("abi 4").  Revision 2 changed index_out to uint32_t, gave
  * pdht_bucket_workspace_bytes its keysize and the *_var_dev entry points
- * their nbytes: a caller built against an older header must be rebuilt. */
-#define PDHT_HIP_ABI_VERSION 3
+ * their nbytes; revision 4 sizes the workspace of pdht_bucket_records_dev by
+ * pdht_bucket_records_workspace_bytes (array callers no longer reserve the
+ * records' two-pass region): a caller built against an older header must be
+ * rebuilt. */
+#define PDHT_HIP_ABI_VERSION 4
 
 typedef struct ihipStream_t *pdht_hip_stream_t; /* layout of hipStream_t */
 
@@ -120,8 +123,8 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * ptindex_out is best NULL.  nranks <= 8192, n < 2^32.  `workspace`
  * (device) must hold pdht_bucket_workspace_bytes(n, keysize, nranks): the
  * per-tile counts and, for 8/16/32-B keys at the rank counts that take the
- * two-pass sort (from 1536 / 1025 / 1025 ranks for 8 / 16 / 32-B keys; 32-B
- * arrays take it from 2049), its intermediate (n x (keysize + 4) bytes). */
+ * two-pass sort (from 1536 / 1025 / 2049 ranks for 8 / 16 / 32-B keys), its
+ * intermediate (about n x (keysize + 4) bytes). */
 size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint32_t nptes, uint32_t nranks, void *workspace,
@@ -143,10 +146,15 @@ int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
  *                          (message_t's alignment padding)
  *   +16 uint64 mbits     = CityHash64(key)
  *   +24 key[keysize], zero-padded to the stride.
- * records (device, 8-byte aligned) holds n records; bucket_offsets and the
- * workspace as for pdht_bucket_batch_dev.  ptindex is not stored (it is
+ * records (device, 8-byte aligned) holds n records; bucket_offsets as for
+ * pdht_bucket_batch_dev, the workspace sized by
+ * pdht_bucket_records_workspace_bytes.  ptindex is not stored (it is
  * mbits % nptes; the MPI message carries ht_index instead). */
 size_t pdht_bucket_record_bytes(size_t keysize);
+/* Workspace of pdht_bucket_records_dev: as pdht_bucket_workspace_bytes, with
+ * the records' two-pass thresholds (32-B keys from 1025 ranks instead of
+ * 2049); never smaller than the array query. */
+size_t pdht_bucket_records_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n,
                             uint32_t nranks, uint32_t msg_type, uint32_t src_rank,
                             uint32_t ht_index, void *workspace,

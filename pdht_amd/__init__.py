@@ -112,6 +112,7 @@ def _declare(L, tuning=False):
         "pdht_hip_key_stream_dev": (C.c_int, [_V, _S, _V, _V]),
         "pdht_hip_key_stream_var_dev": (C.c_int, [_V, _S, _V, _S, _V, _V]),
         "pdht_bucket_workspace_bytes": (C.c_size_t, [_S, _S, _U32]),
+        "pdht_bucket_records_workspace_bytes": (C.c_size_t, [_S, _S, _U32]),
         "pdht_bucket_batch_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _V, _S, _V, _V, _V, _V, _V, _V]),
         "pdht_bucket_record_bytes": (C.c_size_t, [_S]),
         "pdht_bucket_records_dev": (C.c_int, [_V, _S, _S, _U32, _U32, _U32, _U32, _V, _S, _V, _V, _V]),
@@ -177,7 +178,8 @@ def mpi_lib():
 
 class tuning:
     """Context manager for tools/ and the A/B tests: route every wrapper
-    through libpdht_hip_tuning.so (same sources, -DPDHT_HIP_TUNING) with
+    through libpdht_hip_tuning.so (same sources, built with the A/B hook
+    headers of pdht_amd/csrc/tuning/) with
     kernel variant `variant` and, optionally, `per_cu` workgroups per CU.
     The product library has no variants and no tuning entry points."""
 
@@ -588,13 +590,17 @@ def bind_place_batch(keys, nptes: int, nranks: int, *, hist=None, stream=None, o
     return call, out
 
 
-def bucket_workspace_bytes(n: int, keysize: int, nranks: int) -> int:
+def bucket_workspace_bytes(n: int, keysize: int, nranks: int, records: bool = False) -> int:
+    """Workspace bytes of bucket_batch (records=False) or bucket_records
+    (records=True) on n keysize-byte keys over nranks ranks."""
+    if records:
+        return lib().pdht_bucket_records_workspace_bytes(n, keysize, nranks)
     return lib().pdht_bucket_workspace_bytes(n, keysize, nranks)
 
 
-def _workspace(workspace, n, L, nranks, dev):
+def _workspace(workspace, n, L, nranks, dev, records=False):
     torch = _torch()
-    need = lib().pdht_bucket_workspace_bytes(n, L, nranks)
+    need = bucket_workspace_bytes(n, L, nranks, records)
     if workspace is None:
         return torch.empty(max(need, 1), dtype=torch.uint8, device=dev), need
     _need(workspace, "workspace", torch.uint8, dev, numel=need)
@@ -657,7 +663,8 @@ def bucket_records(keys, nranks: int, *, msg_type: int = PDHT_PUT, src_rank: int
 
     Returns (records uint8 [n, pdht_bucket_record_bytes(L)], offsets int64
     [nranks+1]); record_fields() splits them into tensors.  `out` = a previous
-    return value to reuse; `workspace` as for bucket_batch.
+    return value to reuse; `workspace` as for bucket_batch, of at least
+    bucket_workspace_bytes(n, L, nranks, records=True) bytes.
     """
     torch = _torch()
     n, L, stride = _keys_2d(keys)
@@ -665,7 +672,7 @@ def bucket_records(keys, nranks: int, *, msg_type: int = PDHT_PUT, src_rank: int
         raise ValueError("bucket_records needs packed keys")
     dev = keys.device
     rb = bucket_record_bytes(L)
-    ws, ws_bytes = _workspace(workspace, n, L, nranks, dev)
+    ws, ws_bytes = _workspace(workspace, n, L, nranks, dev, records=True)
     if out is not None:
         rec, offs = out
         _need(rec, "out[0] (records)", torch.uint8, dev, shape=(n, rb))

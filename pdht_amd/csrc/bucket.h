@@ -1091,6 +1091,279 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
   }
 }
 
+// -------------------------------------- two-pass bucketing, tile-local runs ---
+// r06 restructure of the two passes.  Above, pass 1
+// writes each tile's fine-bucket runs to GLOBAL fine-bucket positions, so it
+// needs every tile's fine counts scanned first: a counting kernel reads and
+// hashes the whole batch once more ahead of it (count + scans: ~57 of 336 us
+// at 8192 ranks).  Here pass 1 needs nothing ahead of it:
+//   pass 1 (k_bucket_tl_pass1): per tile of TILE keys (one sub-tile), sort by
+//          the fine digit f in LDS and write the tile back IN PLACE -- rows
+//          [t*TILE, (t+1)*TILE) of the intermediate, one contiguous store run
+//          per wave instruction -- as key rows + the u16 index inside the
+//          tile, plus the tile's F run starts (u16) startsF[t][f].  Per
+//          count-chunk of ct tiles it also keeps the rank histogram (u16
+//          pairs in LDS) -> chunkcnt[g][r]: the counting the old count kernel
+//          did, without a second read of the keys;
+//   scans: chunkcnt down the chunks per rank (k_bucket_chunkscan) + bucket
+//          bases (k_bucket_base);
+//   pass 2 (k_bucket_tl_pass2): per segment = (f, a range of count-chunks),
+//          GATHER the f-runs of the segment's tiles (each run ~TILE / F
+//          keys, contiguous) through an LDS row map, sort by the coarse
+//          digit c and store every output at its final slot (as
+//          k_bucket_pass2 does).  Original index = tile row base | u16.
+// One launch fewer, no second hash of the batch, pass-1 stores whole lines;
+// the intermediate shrinks from L + 4 to L + 2 bytes per key.
+constexpr u32 kTlMaxRuns = 512;  // tiles (= f-runs) per pass-2 segment
+struct TwoPassTL {
+  u32 fbits, F, C, cbits;
+  u32 tshift;                 // log2 keys per pass-1 tile
+  u32 ct;                     // tiles per count-chunk
+  u64 n, ntiles, nchunks;
+  u64 nsegf, nseg;            // segments per fine bucket; segments
+  u32 sgmajor;                // segment order: 0 = f-major (all of f, then f + 1), 1 = chunk-range-major
+  uint16_t *startsF;          // [ntiles][F] tile-local first row of fine bucket f
+  u32 *chunkcnt;              // [nchunks][nranks] rank histogram of chunk g; after the scan its exclusive prefix
+  const u64 *base;            // [nranks] first final slot of bucket r
+  uint8_t *ikeys;             // [n][L] key rows, each tile sorted by f in place
+  uint16_t *ilidx;            // [n] index of the row's key inside its tile
+  __device__ __forceinline__ u32 tile_n(u64 t) const {
+    const u64 b = t << tshift;
+    return (u32)min((u64)1 << tshift, n - b);
+  }
+};
+
+template <int W, int KPL>
+constexpr size_t tl_pass1_lds_bytes(u32 nranks) {
+  return (size_t)W * KPL * 64 * (8 + 2) + (size_t)((nranks + 1) / 2) * 4;
+}
+template <int W, int KPL>
+constexpr size_t tl_pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
+
+template <int L, int W, int KPL, int WPE>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_bucket_tl_pass1(const uint8_t *__restrict__ keys, FastMod rk, u32 nranks, TwoPassTL tp) {
+  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
+  static_assert(kTile <= 8192 && (kTile & (kTile - 1)) == 0, "u16 tile rows; power-of-two tiles");
+  extern __shared__ u64 lds64[];
+  u64 *stage = lds64;                                            // [kTile] key pieces in f order
+  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile] tile-local index in f order
+  u32 *hist = reinterpret_cast<u32 *>(sidx + kTile);            // [(nranks+1)/2] u16 pairs: the chunk's ranks
+  __shared__ u32 runt[W * kTpMaxDigits];
+  __shared__ u32 scan_scratch[W];
+  const RunTab<false> run{runt, tp.F};
+  const u32 fmask = tp.F - 1;
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u32 q0 = wave * kSub + lane;
+  const u32 hw = (nranks + 1) / 2;
+  const u64 n = tp.n;
+  for (TileOrder o(tp.nchunks); o.t < o.end; o.t += o.step) {
+    const u64 g = o.t;
+    for (u32 j = threadIdx.x; j < hw; j += kB) hist[j] = 0;
+    __syncthreads();  // (once per chunk) the rank counts below may start right after the hash
+    const u64 t1 = min((g + 1) * tp.ct, tp.ntiles);
+    for (u64 t = g * tp.ct; t < t1; ++t) {
+      const u64 tbase = t * kTile;
+      const u32 tn = (u32)min((u64)kTile, n - tbase);
+      for (u32 j = threadIdx.x; j < W * tp.F; j += kB) runt[j] = 0;
+      RegReader<L / 4> kr[KPL];
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) load_key_regs<L, true>(keys, min(tbase + q0 + k * 64, n - 1), kr[k]);
+      u32 ff[KPL];
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const u32 r = (u32)rk.mod(city64(kr[k], (u64)L));
+        ff[k] = r & fmask;
+        if (q0 + k * 64 < tn) atomicAdd(&hist[r >> 1], 1u << (16 * (r & 1)));
+      }
+      __syncthreads();  // runt zeroed; the previous tile's stage / sidx reads done
+#pragma unroll
+      for (int k = 0; k < KPL; ++k)
+        if (q0 + k * 64 < tn) run.add(wave, ff[k], 1u);
+      __syncthreads();
+      {  // the tile's f-run starts: out to startsF, and each wave's first slot of every f
+        const u32 d = threadIdx.x;
+        u32 s = 0;
+        if (d < tp.F)
+#pragma unroll
+          for (int w = 0; w < W; ++w) s += run.get(w, d);
+        u32 acc = block_exclusive_scan<W>(s, scan_scratch);
+        if (d < tp.F) {
+          tp.startsF[t * tp.F + d] = (uint16_t)acc;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const u32 v = run.get(w, d);
+            run.set(w, d, acc);
+            acc += v;
+          }
+        }
+      }
+      __syncthreads();
+      u32 lp[KPL];
+      rank_groups<KPL>(run, wave, ff, q0, tn, tp.fbits, lp);
+#pragma unroll
+      for (int k = 0; k < KPL; ++k)
+        if (q0 + k * 64 < tn) {
+          stage[lp[k]] = (u64)kr[k].d[0] | ((u64)kr[k].d[1] << 32);
+          sidx[lp[k]] = (uint16_t)(q0 + k * 64);
+        }
+      __syncthreads();
+#pragma unroll
+      for (int jj = 0; jj < KPL; ++jj) {
+        const u32 j = jj * kB + threadIdx.x;
+        if (j < tn) {
+          *reinterpret_cast<u64 *>(tp.ikeys + (tbase + j) * L) = stage[j];
+          tp.ilidx[tbase + j] = sidx[j];
+        }
+      }
+#pragma unroll
+      for (int c = 1; c < L / 8; ++c) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPL; ++k)
+          if (q0 + k * 64 < tn) stage[lp[k]] = (u64)kr[k].d[2 * c] | ((u64)kr[k].d[2 * c + 1] << 32);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < KPL; ++jj) {
+          const u32 j = jj * kB + threadIdx.x;
+          if (j < tn) *reinterpret_cast<u64 *>(tp.ikeys + (tbase + j) * L + 8 * c) = stage[j];
+        }
+      }
+    }
+    __syncthreads();  // every atomic of the chunk is in
+    for (u32 r = threadIdx.x; r < nranks; r += kB) tp.chunkcnt[g * nranks + r] = (hist[r >> 1] >> (16 * (r & 1))) & 0xffffu;
+    __syncthreads();
+  }
+}
+
+// PROBE (A/B timing only, wrong outputs): 1 = every sub-tile reads its rows
+// contiguously from row o.t * 3840 instead of through the row map (what the
+// gather costs).
+template <int L, class Out, int W, int KPL, int WPE, bool ONE = (L == 8 && !Out::kPair8), int PROBE = 0>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_bucket_tl_pass2(FastMod rk, u32 nranks, TwoPassTL tp, Out out) {
+  static_assert(!ONE || (L == 8 && !Out::kPair8), "one store phase: 8-B keys into arrays");
+  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
+  constexpr u32 RP = (kTlMaxRuns + kB - 1) / kB;  // runs per thread
+  extern __shared__ u64 lds64[];
+  u64 *stage = lds64;                                  // [kTile] digests / key pieces
+  u32 *sidx = reinterpret_cast<u32 *>(stage + kTile);  // [kTile] source rows of the sub-tile, then original indices
+  __shared__ u32 runt[W * kTpMaxDigits];
+  __shared__ u32 running[kTpMaxDigits];  // next final slot of bucket c*F + f
+  __shared__ u32 delta[kTpMaxDigits];
+  __shared__ u32 tcount[kTpMaxDigits];
+  __shared__ u32 scan_scratch[W];
+  __shared__ u32 s_len;
+  const RunTab<false> run{runt, tp.C};
+  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u32 q0 = wave * kSub + lane;
+  const u32 fbits = tp.fbits;
+  const u32 tmask = (1u << tp.tshift) - 1;
+  auto coarse = [&](u64 h, u32) { return (u32)rk.mod(h) >> fbits; };
+  for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
+    // the count-chunks split evenly over the nsegf segments of f
+    const u32 f = tp.sgmajor ? (u32)(o.t % tp.F) : (u32)(o.t / tp.nsegf);
+    const u64 sg = tp.sgmajor ? o.t / tp.F : o.t % tp.nsegf;
+    const u64 g0 = sg * tp.nchunks / tp.nsegf, g1 = (sg + 1) * tp.nchunks / tp.nsegf;
+    const u64 ta = g0 * tp.ct, tb = min(g1 * tp.ct, tp.ntiles);
+    // this thread's runs: tiles ta + threadIdx.x * RP + q (contiguous, so a
+    // block scan of the per-thread sums orders them by tile)
+    u32 src[RP], cnt[RP], pos[RP];
+    u32 mine = 0;
+#pragma unroll
+    for (int q = 0; q < RP; ++q) {
+      const u64 t = ta + (u64)threadIdx.x * RP + q;
+      src[q] = cnt[q] = 0;
+      if (t < tb) {
+        const u32 s = tp.startsF[t * tp.F + f];
+        const u32 e = f + 1 < tp.F ? tp.startsF[t * tp.F + f + 1] : tp.tile_n(t);
+        src[q] = (u32)(t << tp.tshift) + s;
+        cnt[q] = e - s;
+      }
+      pos[q] = mine;
+      mine += cnt[q];
+    }
+    if (threadIdx.x < tp.C) {
+      const u32 r = threadIdx.x * tp.F + f;
+      if (r < nranks) running[threadIdx.x] = (u32)tp.base[r] + tp.chunkcnt[g0 * nranks + r];
+    }
+    const u32 before = block_exclusive_scan<W>(mine, scan_scratch);
+#pragma unroll
+    for (int q = 0; q < RP; ++q) pos[q] += before;
+    if (threadIdx.x == kB - 1) s_len = before + mine;
+    __syncthreads();
+    const u32 slen = s_len;
+    for (u32 k0 = 0; k0 < slen; k0 += kTile) {
+      const u32 tn = min(kTile, slen - k0);
+      // the sub-tile's row map: sidx[p - k0] = intermediate row of segment key p
+#pragma unroll
+      for (int q = 0; q < RP; ++q) {
+        const u32 lo = max(pos[q], k0), hi = min(pos[q] + cnt[q], k0 + tn);
+        for (u32 p = lo; p < hi; ++p) sidx[p - k0] = src[q] + (p - pos[q]);
+      }
+      for (u32 j = threadIdx.x; j < W * tp.C; j += kB) runt[j] = 0;
+      __syncthreads();
+      RegReader<L / 4> kr[KPL];
+      u32 ix[KPL];
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const u32 row = PROBE == 1 ? (u32)((o.t * 3840 + k0 + min(q0 + k * 64, tn - 1)) % tp.n)
+                                   : sidx[min(q0 + k * 64, tn - 1)];
+        load_key_regs<L, true>(tp.ikeys, row, kr[k]);
+        ix[k] = (row & ~tmask) | (u32)__builtin_nontemporal_load(tp.ilidx + row);
+      }
+      u64 h[ONE ? 1 : KPL];
+      u32 cc[KPL];
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const u64 hh = city64(kr[k], (u64)L);
+        if constexpr (!ONE) h[k] = hh;
+        cc[k] = coarse(hh, 0u);
+      }
+      __syncthreads();  // the row map is read
+#pragma unroll
+      for (int k = 0; k < KPL; ++k)
+        if (q0 + k * 64 < tn) run.add(wave, cc[k], 1u);
+      __syncthreads();
+      digit_starts<W>(run, tp.C, delta, tcount, scan_scratch, [&](u32 c) { return running[c]; });
+      __syncthreads();
+      u32 lp[KPL];
+      rank_groups<KPL>(run, wave, cc, q0, tn, tp.cbits, lp);
+#pragma unroll
+      for (int k = 0; k < KPL; ++k)
+        if (q0 + k * 64 < tn) {
+          if constexpr (ONE)
+            stage[lp[k]] = (u64)kr[k].d[0] | ((u64)kr[k].d[1] << 32);
+          else
+            stage[lp[k]] = h[k];
+          sidx[lp[k]] = ix[k];
+        }
+      __syncthreads();
+      if constexpr (ONE) {
+#pragma unroll
+        for (int jj = 0; jj < KPL; ++jj) {
+          const u32 j = jj * kB + threadIdx.x;
+          if (j < tn) {
+            RegReader<2> r;
+            const u64 key = stage[j];
+            r.d[0] = (u32)key;
+            r.d[1] = (u32)(key >> 32);
+            const u64 hv = city64(r, (u64)L);
+            const u32 slot = delta[coarse(hv, 0u)] + j;
+            out.meta(slot, hv, sidx[j]);
+            if (out.has_keys()) out.key8(slot, 0, key);
+          }
+        }
+      } else {
+        staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
+      }
+      __syncthreads();
+      if (threadIdx.x < tp.C) running[threadIdx.x] += tcount[threadIdx.x];
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------- generic-length scatter ---
 // Tile = W waves x 32 groups; wave w owns a contiguous 2048-key sub-range.
 // Counting pass hashes; the scatter pass hashes again from L2-resident keys

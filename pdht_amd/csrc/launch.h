@@ -8,9 +8,8 @@ namespace pdht {
 
 constexpr int kWinBytes = 12288;  // k_window over fixed keys: LDS window per wave (12 KiB)
 }  // namespace pdht
-#ifdef PDHT_HIP_TUNING
-#include "tuning/launch_tuning.h"  // the A/B harness's alternative shapes: one hook per path below
-#endif
+// one A/B hook per launch path below (product/pdht_hooks_launch.h: none taken)
+#include "pdht_hooks_launch.h"
 namespace pdht {
 // Kernel tags (pdht_hip_last_kernel): the kernel and its launch shape, so a
 // profile taken of one shape (profiles/traffic_*.json) is never attributed to
@@ -34,9 +33,7 @@ static void launch_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, S
                          hipStream_t st, int dev, u64 blocks) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt snt = NtSink<Sink>::make(sink);
-#ifdef PDHT_HIP_TUNING
-  if (tuning_small(keylen, k, n, algo, sink, st, dev, blocks) != kNoVariant) return;
-#endif
+  if (hook_small(keylen, k, n, algo, sink, st, dev, blocks) != kNoVariant) return;
   if constexpr (std::is_same<Sink, SinkPlace>::value) {
     // With a histogram: 1024-thread workgroups, 2 per CU.  Every workgroup
     // flushes its LDS bins with one device-scope atomic per bin, and those
@@ -104,12 +101,7 @@ static bool sink_has_hist(const Sink &s) {
 //   256 MiB             1.592                     0.2011
 // (cfg3's window kernel is indifferent: 1.92 ms at 0.5-2 GiB, 1.94 in one.)
 constexpr u64 kLaunchBytes = 512ull << 20;
-static u64 launch_chunk_bytes() {
-#ifdef PDHT_HIP_TUNING
-  if (const u64 b = tuning_chunk_bytes()) return b;
-#endif
-  return kLaunchBytes;
-}
+static u64 launch_chunk_bytes() { return hook_chunk_bytes(kLaunchBytes); }
 
 template <class Algo, class Sink>
 static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
@@ -157,10 +149,8 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
   // the CRC-table algorithms serve keys > 900 B only: window / global kernels
   constexpr bool kShort = !HasCrcLds<Algo>::value;
   if (kShort && packed && keylen == 64 && al16) {
-#ifdef PDHT_HIP_TUNING
     if constexpr (kShort)
-      if (int rc = tuning_xpose64(k, n, algo, sink, st, dev); rc != kNoVariant) return rc;
-#endif
+      if (int rc = hook_xpose64(k, n, algo, sink, st, dev); rc != kNoVariant) return rc;
     // measured fastest (profiles/r01/kbench_*): non-temporal loads
     // and stores, two tiles of prefetch in flight per wave, 3 workgroups/CU.
     // Placement with a histogram on up to 4M keys: 1024-thread workgroups, 1
@@ -189,10 +179,7 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
     // window): per-lane global reads, the 6-bit tables in LDS, 8 WG/CU
     // (VGPR-bound to 3 waves per SIMD)
     const unsigned g = grid_for(blocks, 8, dev);
-#ifdef PDHT_HIP_TUNING
-    if (al16 && stride % 16 == 0)
-      if (int rc = tuning_crc_long(k, stride, keylen, n, algo, sink, st, dev, blocks); rc != kNoVariant) return rc;
-#endif
+    if (int rc = hook_crc_long(k, stride, keylen, n, algo, sink, st, dev, blocks); rc != kNoVariant) return rc;
     if (al16 && stride % 16 == 0) {
       g_kernel = "k_global<fixed,a16,lines>@8";
       k_global<false, Algo, SinkNt, true, kLongLines><<<g, kBlock, 0, st>>>(k, nullptr, 0, stride, keylen, n,
@@ -214,10 +201,8 @@ static int launch_fixed_one(const void *keys, size_t stride, size_t keylen, size
       // against 0.535 at 8)
       constexpr int kPerCu = 2;
       if (al16 && stride % 16 == 0) {
-#ifdef PDHT_HIP_TUNING
-        if (int rc = tuning_long_walk(k, stride, keylen, n, algo, sink, st, dev, blocks, kPerCu); rc != kNoVariant)
+        if (int rc = hook_long_walk(k, stride, keylen, n, algo, sink, st, dev, blocks, kPerCu); rc != kNoVariant)
           return rc;
-#endif
         g_kernel = "k_global<fixed,a16,lines>@2";
         k_global<false, Algo, SinkNt, true, kLongLines><<<grid_for(blocks, kPerCu, dev), kBlock, 0, st>>>(
             k, nullptr, 0, stride, keylen, n, algo, sink_nt);
@@ -285,9 +270,7 @@ static int launch_var_one(const void *bytes, u64 nbytes, const u64 *offsets, u64
   const SinkNt sink_nt = NtSink<Sink>::make(sink);
   const u64 wb = ((n + 63) / 64 + 3) / 4;  // blocks of 4 wave-tiles
   bool wide = nbytes / n > 160;
-#ifdef PDHT_HIP_TUNING
-  if (int rc = tuning_var(b, offsets, obase, n, algo, sink, st, dev, wb, wide); rc != kNoVariant) return rc;
-#endif
+  if (int rc = hook_var(b, offsets, obase, n, algo, sink, st, dev, wb, wide); rc != kNoVariant) return rc;
   if (wide) {
     g_kernel = "k_window<var,nt,16K>@2";
     k_window<16384, true, Algo, SinkNt, 2><<<grid_for(wb, 2, dev), kBlock, 0, st>>>(b, offsets, obase, 0, 0, n,

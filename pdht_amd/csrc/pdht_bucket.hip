@@ -20,6 +20,12 @@ struct BucketWs {
   u64 *totalsF;
   uint8_t *ikeys;
   u32 *iidx;
+  // the tile-local two-pass sort (r06, bucket.h k_bucket_tl_*) in the same
+  // region: per-tile f-run starts, per-chunk rank histograms, key rows and
+  // their u16 indices inside the tile
+  uint16_t *tl_starts, *tl_lidx;
+  u32 *tl_chunkcnt;
+  uint8_t *tl_keys;
   size_t bytes;
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -35,17 +41,25 @@ static bool two_pass_keysize(size_t keysize) { return keysize == 8 || keysize ==
 static u32 two_pass_min_ranks(size_t keysize, bool records) {
   return keysize == 8 ? 1536 : keysize == 16 ? 1025 : records ? 1025 : 2049;
 }
-// the workspace (sized without knowing the output kind) reserves the
-// intermediate from the lower of the two thresholds
-static u32 two_pass_reserve_ranks(size_t keysize) {
-  return std::min(two_pass_min_ranks(keysize, false), two_pass_min_ranks(keysize, true));
+// Tile-local two-pass sort (r06, bucket.h k_bucket_tl_*): pass-1 tiles of
+// 4096 keys (2048 for 32-B keys: 8 waves x 4 keys per lane, spill-free), one
+// sub-tile each; count-chunks of ct tiles, ct the largest power of two <= 8
+// that still leaves >= 512 chunks (two pass-1 workgroups on each of 256
+// CUs), so that a chunk's histogram never counts past 32768 keys (u16 halves
+// in LDS).  Both depend on n only, so the workspace size does too.
+static u32 tl_tile_shift(size_t keysize) { return hook_tl_tile_shift(keysize == 32 ? 11 : 12, keysize); }
+static u32 tl_chunk_tiles(u64 ntiles, u32 tshift) {
+  u32 ct = std::min<u32>(8, 32768u >> tshift);
+  while (ct > 1 && ntiles / ct < 512) ct >>= 1;
+  return ct;
 }
 // Sized for the smallest tile any scatter kernel uses, plus the two-pass
-// intermediate when the batch can take that path: 8/16/32-B keys from
-// two_pass_min_ranks() up (the tuning build forces two passes at any nranks
-// and always reserves it).  16M x 8-B keys at 1024 ranks: 17 MB; from 1536
-// ranks + 192 MB.
-static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
+// region when the batch can take that path: 8/16/32-B keys from
+// two_pass_min_ranks() up for the output kind (records: `records`; the tuning
+// build forces two passes at any nranks and always reserves it).  The region
+// holds either two-pass form (the r02-r05 one for the A/B build).  16M x 8-B
+// keys at 1024 ranks: 17 MB; from 1536 ranks + 160 MB.
+static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks, bool records) {
   const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   BucketWs w{};
@@ -63,26 +77,41 @@ static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks) {
   off += round256((size_t)kTpMaxDigits * 8);
   w.tickets = reinterpret_cast<u32 *>(p + off);
   off += 256;
-#ifdef PDHT_HIP_TUNING
-  const bool two_pass = two_pass_keysize(keysize);
-#else
-  const bool two_pass = two_pass_keysize(keysize) && nranks >= two_pass_reserve_ranks(keysize);
-#endif
+  const bool two_pass = hook_bucket_reserve(
+      two_pass_keysize(keysize) && nranks >= two_pass_min_ranks(keysize, records), keysize);
   if (two_pass) {
+    // the r02-r05 form: fine counts per tile and chunk, fine totals, rank
+    // counts per chunk, key rows + u32 original indices
+    size_t o = off;
     const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
     const u64 tp_chunks = (tp_tiles + kTpChunkTiles - 1) / kTpChunkTiles;
-    w.countsF = reinterpret_cast<u32 *>(p + off);
-    off += round256((size_t)tp_tiles * kTpMaxDigits * 4);
-    w.chunksF = reinterpret_cast<u32 *>(p + off);  // rows of kTpChunkTiles (or kBucketChunk) tiles
-    off += round256((size_t)tp_chunks * kTpMaxDigits * 4);
-    w.totalsF = reinterpret_cast<u64 *>(p + off);
-    off += round256((size_t)kTpMaxDigits * 8);
-    w.chunkcnt = reinterpret_cast<u32 *>(p + off);
-    off += round256((size_t)tp_chunks * nranks * 4);
-    w.ikeys = p + off;
-    off += round256(n * keysize);
-    w.iidx = reinterpret_cast<u32 *>(p + off);
-    off += round256(n * 4);
+    w.countsF = reinterpret_cast<u32 *>(p + o);
+    o += round256((size_t)tp_tiles * kTpMaxDigits * 4);
+    w.chunksF = reinterpret_cast<u32 *>(p + o);  // rows of kTpChunkTiles (or kBucketChunk) tiles
+    o += round256((size_t)tp_chunks * kTpMaxDigits * 4);
+    w.totalsF = reinterpret_cast<u64 *>(p + o);
+    o += round256((size_t)kTpMaxDigits * 8);
+    w.chunkcnt = reinterpret_cast<u32 *>(p + o);
+    o += round256((size_t)tp_chunks * nranks * 4);
+    w.ikeys = p + o;
+    o += round256(n * keysize);
+    w.iidx = reinterpret_cast<u32 *>(p + o);
+    o += round256(n * 4);
+    // the tile-local form over the same bytes: f-run starts per tile, rank
+    // counts per chunk, key rows + u16 indices inside the tile
+    size_t q = off;
+    const u32 sh = tl_tile_shift(keysize);
+    const u64 tl_tiles = (n + (1ull << sh) - 1) >> sh;
+    const u64 tl_chunks = (tl_tiles + tl_chunk_tiles(tl_tiles, sh) - 1) / tl_chunk_tiles(tl_tiles, sh);
+    w.tl_starts = reinterpret_cast<uint16_t *>(p + q);
+    q += round256((size_t)tl_tiles * kTpMaxDigits * 2);
+    w.tl_chunkcnt = reinterpret_cast<u32 *>(p + q);
+    q += round256((size_t)tl_chunks * nranks * 4);
+    w.tl_keys = p + q;
+    q += round256(n * keysize);
+    w.tl_lidx = reinterpret_cast<uint16_t *>(p + q);
+    q += round256(n * 2);
+    off = std::max(o, q);
   }
   w.bytes = off;
   return w;
@@ -172,6 +201,47 @@ static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &ou
   return 0;
 }
 
+// The tile-local two-pass sort (bucket.h k_bucket_tl_*): pass 1 (sorts
+// each tile by f in place, counts ranks per chunk), the rank scan down the
+// chunks, the bucket bases, pass 2 (gathers the f-runs of each segment, sorts
+// by c, stores at the final slots).  Pass 1 in W1 x KPL1 (one tile) @ PER_CU1,
+// pass 2 in W x KPL @ PER_CU.
+template <int L, class Out, int W, int KPL, int PER_CU, int W1, int KPL1, int PER_CU1, int PROBE = 0>
+static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
+                     uint64_t *bucket_offsets, hipStream_t st, int dev) {
+  static const char *const names[3] = {"k_bucket_tl_pass2<8B>", "k_bucket_tl_pass2<16B>",
+                                       "k_bucket_tl_pass2<32B>"};
+  if ((1u << tl.tshift) != (u32)(W1 * KPL1 * 64)) return fail("tile-local pass 1: tile/shape mismatch%s", "");
+  constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;
+  constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;
+  const size_t b1 = tl_pass1_lds_bytes<W1, KPL1>(a.nranks), b2 = tl_pass2_lds_bytes<W, KPL>();
+  auto f1 = &k_bucket_tl_pass1<L, W1, KPL1, WPE1>;
+  auto f2 = &k_bucket_tl_pass2<L, Out, W, KPL, WPE, (L == 8 && !Out::kPair8), PROBE>;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
+  if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
+  const u64 cus = (u64)std::max(1, g_dev[dev].cus);
+  unsigned g1 = (unsigned)std::min<u64>(tl.nchunks, cus * PER_CU1);
+  if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous chunk order (TileOrder)
+  f1<<<g1, W1 * 64, b1, st>>>(a.k, a.rk, a.nranks, tl);
+  k_bucket_chunkscan<<<(a.nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(tl.chunkcnt, tl.nchunks, a.nranks, w.totals);
+  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, a.nranks, w.base, bucket_offsets, tl.fbits, nullptr, nullptr,
+                                            nullptr);
+  unsigned g2 = (unsigned)std::min<u64>(tl.nseg, cus * PER_CU);
+  if (g2 >= 8) g2 &= ~7u;
+  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tl, out);
+  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
+  return 0;
+}
+
+enum class BucketKernel { kStaged, kGeneric, kTwoPass };
+enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16 };
+}  // namespace pdht
+
+// A/B hook points of the choices below (product/pdht_hooks_bucket.h: none
+// taken)
+#include "pdht_hooks_bucket.h"
+
+namespace pdht {
 template <int L, class Out>
 static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
   // Shapes (waves x keys per lane per sub-tile @ workgroups per CU).  r02's
@@ -186,31 +256,7 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
   // 8-B keys into arrays store from one phase (k_bucket_pass2 ONE) and take
   // pass 2 in 8 x 8 @ 2 as well (4 x 8 @ 4 with ONE: equal to the two-phase
   // product; 8 x 8 @ 2: -1.0 to -1.3 %, profiles/r05/ab/bucket8k_*.log).
-#ifdef PDHT_HIP_TUNING
-  // (r04's shape search, tuning 192-201, removed in r05)
-  constexpr int kW = L == 8 && !Out::kPair8 ? 1 : 0;  // (ONE exists for 8-B arrays only)
-  if (tuning_variant() == 202)  // r02-r03: 4 x 8 @ 4 both, pass 2 storing in two phases
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, kTpW, kTpKPL, kTpPerCu, false>(a, tp, out, st, dev);
-  if (kW && tuning_variant() == 265)  // r04-r05 product for 8-B arrays: pass 2 two-phase 4 x 8 @ 4
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2, false>(a, tp, out, st, dev);
-  if (kW && tuning_variant() == 266)  // ONE in 4 x 8 @ 4
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
-  if constexpr (L >= 16) {  // r05 spill probe (16/32-B keys in 4 keys per lane) and the r04-r05 shapes
-    switch (tuning_variant()) {
-      case 267: return launch_two_pass<L, Out, 8, 4, 2, 8, 4, 2>(a, tp, out, st, dev);
-      case 268: return launch_two_pass<L, Out, 4, 4, 4, 8, 4, 2>(a, tp, out, st, dev);
-      case 269: return launch_two_pass<L, Out, 8, 4, 2, 4, 8, 4>(a, tp, out, st, dev);
-      case 270:
-        if constexpr (L == 16) return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
-        else return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
-      default: break;
-    }
-  }
-  if constexpr (L == 8 && Out::kPair8) {  // 8-B records' pass 2: 4 x 4 @ 4 / r04-r05's 4 x 8 @ 4
-    if (tuning_variant() == 271) return launch_two_pass<L, Out, 4, 4, 4, 8, 8, 2>(a, tp, out, st, dev);
-    if (tuning_variant() == 272) return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
-  }
-#endif
+  if (int rc = hook_two_pass_shape<L, Out>(a, tp, out, st, dev); rc != kNoVariant) return rc;
   // Late r05: at 8 keys per lane the 16/32-B kernels spilled VGPRs (pass 1
   // of 32-B keys 78 registers, pass 2 58); in 4 keys per lane none spill
   // (profiles/r05/ab/bucket_16_32_two_pass_shapes.log, 16M keys): 32-B arrays
@@ -229,9 +275,106 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
     return launch_two_pass<L, Out, 8, 4, 2, 8, 8, 2>(a, tp, out, st, dev);
 }
 
-enum class BucketKernel { kStaged, kGeneric, kTwoPass };
+// Tile-local shapes: pass 1 one tile per sub-tile (8 waves x 8 keys per
+// lane = 4096 keys; 32-B keys 8 x 4 = 2048, spill-free) at 2 WG/CU; pass 2
+// the shapes the r02-r05 pass 2 measured best per key size and output kind
+// (launch_two_pass_sel).
+template <int L, class Out>
+static int launch_tl_sel(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
+                         uint64_t *bucket_offsets, hipStream_t st, int dev) {
+  if (int rc = hook_tl_shape<L, Out>(a, tl, out, w, bucket_offsets, st, dev); rc != kNoVariant) return rc;
+  if constexpr (L == 32 && !Out::kPair8)
+    return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 32)
+    return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 16 && Out::kPair8)
+    return launch_tl<L, Out, 4, 4, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 16 || (L == 8 && !Out::kPair8))
+    return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else
+    return launch_tl<L, Out, 8, 4, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+}
 
-enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16 };
+// The two digits of rank = c * F + f.  Array outputs of 8/16-B keys take one
+// fine bit more than the balanced split (8192 ranks: F = 256, C = 32): pass 2
+// writes 24 / 32 B per key in runs of ~4096 / C keys against pass 1's 12 / 20 B
+// in runs of ~4096 / F, so longer pass-2 runs pay.  Three boxes, 16M keys
+// (profiles/r03/ab/bucket_two_pass_digits.log): 8 B at 8192 ranks -5.5 /
+// 0 / -3.6 %, 16 B at 4096 ranks -4.3 / -4.0 %, 2048 ranks within +-2 %.
+// 32-B keys (pass 1 writes 36 B/key) lose 3 % with it, and records (AoS
+// rows, pass-2 runs already >= 1 KiB) 1 %: both keep the balanced split.
+struct Digits {
+  u32 fbits, F, C, cbits;
+};
+template <class Out>
+static Digits digit_split(u32 nbits, u32 nranks, size_t keysize) {
+  Digits d{};
+  d.fbits = (nbits + 1) / 2;
+  const bool fine_plus = hook_fine_plus(std::is_same<Out, OutSoA>::value && keysize <= 16);
+  if (fine_plus && d.fbits + 1 <= std::min<u32>(8, nbits)) ++d.fbits;
+  d.F = 1u << d.fbits;
+  d.C = (nranks + d.F - 1) >> d.fbits;
+  d.cbits = nbits - d.fbits;
+  return d;
+}
+
+// Pass-2 segments: nsegf per fine bucket, each a run of whole count-chunks
+// (chunk = `chunk_keys` keys, ~chunk_keys / F of them in bucket f), split
+// evenly.  SG chunks make ~kTpSegKeys keys; when the remainder of
+// nchunks / SG leaves at most one extra chunk per segment, take the floor
+// (segments of SG or SG + 1 chunks: ~3968 keys at most) rather than the
+// ceiling, whose segments are ~6 % shorter in the mean but one more per fine
+// bucket -- one more pass through the sub-tile's phase chain (16M keys at
+// 8192 ranks: 17 segments of 30-31 chunks instead of 18).  Interleaved
+// against the ceiling (profiles/r05/ab/bucket_pass2_even_segments.log):
+// 8-B records at 8192 ranks -1.8 %, arrays within +-0.5 %.  PDHT_TP_EVEN_SEG=0
+// (experiment builds): the ceiling.  (Only where SG + 1 chunks stay ~2 sigma
+// under 4096 keys: at F <= 128 one chunk more is 256+ keys and would spill
+// half the time.)
+static void split_segments(u64 nchunks, u64 chunk_keys, u32 F, u64 *SG, u64 *nsegf) {
+  *SG = std::max<u64>(1, (u64)F * kTpSegKeys / chunk_keys);
+  const u64 nfl = std::max<u64>(1, nchunks / *SG);
+  const u64 step = chunk_keys / F;  // keys of one fine bucket per chunk
+  const bool floor_ok = PDHT_TP_EVEN_SEG && (*SG + 1) * step <= 3968 && nchunks - nfl * *SG <= nfl;
+  *nsegf = floor_ok ? nfl : (nchunks + *SG - 1) / *SG;
+}
+
+// The tile-local two-pass bucketing (k_bucket_tl_*), n >= 1.
+template <class Out>
+static int bucket_tl(const BucketArgs &a, const BucketWs &w, size_t keysize, const Out &out,
+                     uint64_t *bucket_offsets, hipStream_t st, int dev) {
+  const Digits d = digit_split<Out>(a.nbits, a.nranks, keysize);
+  if (d.F > kTpMaxDigits || d.C > kTpMaxDigits)  // the kernels' LDS digit tables
+    return fail("two-pass digit split: a digit of %s%lld buckets exceeds the LDS tables", "",
+                (long long)(d.F > kTpMaxDigits ? d.F : d.C));
+  TwoPassTL tl{};
+  tl.fbits = d.fbits;
+  tl.F = d.F;
+  tl.C = d.C;
+  tl.cbits = d.cbits;
+  tl.tshift = tl_tile_shift(keysize);
+  tl.n = a.n;
+  tl.ntiles = (a.n + (1ull << tl.tshift) - 1) >> tl.tshift;
+  tl.ct = tl_chunk_tiles(tl.ntiles, tl.tshift);
+  tl.nchunks = (tl.ntiles + tl.ct - 1) / tl.ct;
+  u64 SG = 0;
+  split_segments(tl.nchunks, (u64)tl.ct << tl.tshift, tl.F, &SG, &tl.nsegf);
+  // a segment's f-runs (one per tile) must fit pass 2's run table
+  const u64 seg_tiles = (tl.nchunks + tl.nsegf - 1) / tl.nsegf * tl.ct;
+  if (seg_tiles > kTlMaxRuns)
+    return fail("tile-local two-pass: %s%lld tiles per segment exceed the run table", "", (long long)seg_tiles);
+  tl.nseg = (u64)tl.F * tl.nsegf;
+  tl.sgmajor = hook_tl_sgmajor(false);
+  tl.startsF = w.tl_starts;
+  tl.chunkcnt = w.tl_chunkcnt;
+  tl.base = w.base;
+  tl.ikeys = w.tl_keys;
+  tl.ilidx = w.tl_lidx;
+  return keysize == 8    ? launch_tl_sel<8, Out>(a, tl, out, w, bucket_offsets, st, dev)
+         : keysize == 16 ? launch_tl_sel<16, Out>(a, tl, out, w, bucket_offsets, st, dev)
+                         : launch_tl_sel<32, Out>(a, tl, out, w, bucket_offsets, st, dev);
+}
+
 template <class Out>
 static StagedShape staged_shape(size_t keysize, u32 nranks) {
   if (nranks < 512) return StagedShape::kBallot4x16;
@@ -250,9 +393,9 @@ static StagedShape staged_shape(size_t keysize, u32 nranks) {
 }
 
 // Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
-// (OutRec): counting pass, scans, bucket bases, then the scatter into `out`.
-// out_al: alignment bits of the output key rows (0 when they are 8-B aligned
-// 8-B pieces, as in records).
+// (OutRec): counting pass, scans, bucket bases, then the scatter into `out`
+// (two passes: bucket_tl).  out_al: alignment bits of the output key rows (0
+// when they are 8-B aligned 8-B pieces, as in records).
 template <class Out>
 static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nranks, void *workspace,
                        size_t workspace_bytes, const Out &out, uintptr_t out_al, uint64_t *bucket_offsets,
@@ -262,7 +405,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   if (n >= (1ull << 32)) return fail("bucketing: n must be < 2^32 per call%s", "");
   if (!bucket_offsets) return fail("bucket_offsets must not be NULL%s", "");
   if (n && (!keys || keysize == 0)) return fail("null keys or zero keysize%s", "");
-  const BucketWs w = bucket_layout(workspace, n, keysize, nranks);
+  const BucketWs w = bucket_layout(workspace, n, keysize, nranks, Out::kPair8);
   if (!workspace || workspace_bytes < w.bytes) return fail("workspace too small%s", "");
   int dev;
   if (int rc = current_device(&dev)) return rc;
@@ -272,34 +415,38 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   const bool fixed = (keysize == 8 && (al & 7) == 0) || ((keysize == 16 || keysize == 32) && (al & 15) == 0);
   // (two_pass_min_ranks <= kStagedMaxRanks + 1: the staged scatter covers
   // every nranks below the two-pass threshold)
-  BucketKernel kind = !fixed                                ? BucketKernel::kGeneric
-                      : nranks >= two_pass_min_ranks(keysize, Out::kPair8) ? BucketKernel::kTwoPass
-                                                              : BucketKernel::kStaged;
-#ifdef PDHT_HIP_TUNING
-  // 21: the generic-length kernel for 8/16/32-B keys too; 70: one pass (the
-  // staged scatter) up to 2048 ranks whatever the two-pass threshold; 71:
-  // two passes at any nranks >= 2.  (r02's gather, producer/consumer and
-  // register scatters measured slower than the staged one and were removed
-  // in r03: DESIGN.md §4.4.)
-  if (tuning_variant() == 70 && kind == BucketKernel::kTwoPass && nranks <= kStagedMaxRanks)
-    kind = BucketKernel::kStaged;
-  if (tuning_variant() == 71 && fixed && nranks >= 2) kind = BucketKernel::kTwoPass;
-  if (tuning_variant() == 21) kind = BucketKernel::kGeneric;
-#endif
+  const BucketKernel kind = hook_bucket_kind(
+      !fixed                                                 ? BucketKernel::kGeneric
+      : nranks >= two_pass_min_ranks(keysize, Out::kPair8) ? BucketKernel::kTwoPass
+                                                             : BucketKernel::kStaged,
+      fixed, nranks);
+  BucketArgs a{};
+  a.k = static_cast<const uint8_t *>(keys);
+  a.n = n;
+  a.rk = make_fastmod(nranks);
+  a.nranks = nranks;
+  while ((1u << a.nbits) < nranks) ++a.nbits;
+  const size_t hist_lds = (size_t)nranks * 4;
+  // Two passes, tile-local form (r06): no counting pass ahead of pass 1
+  if (kind == BucketKernel::kTwoPass && hook_tile_local(true)) {
+    if (n == 0) {
+      HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
+      k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, 0, nullptr, nullptr,
+                                                nullptr);
+      g_kernel = "k_bucket_base";
+    } else if (int rc = bucket_tl(a, w, keysize, out, bucket_offsets, st, dev)) {
+      return rc;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   // Staged scatter shape (tools/abbench.py): owner-table
   // ranking for array outputs from 512 ranks; with it, 8 waves x 16 keys per
   // lane (8192-key tiles, 1 WG/CU) for 8/16-B keys while the LDS holds
   // (8-B keys at 1024 ranks 0.274 -> 0.261 ms, 16-B 0.443 -> 0.405; 32-B
   // keys lose 11 % and keep 4 x 16); else 4 x 16 while two workgroups fit a
   // CU (<= 1462 ranks); ballots below 512 ranks and for records.
-  StagedShape shape = staged_shape<Out>(keysize, nranks);
-#ifdef PDHT_HIP_TUNING
-  // 83 / 87: owner ranking on 8 x 16 / 4 x 16 tiles, 85 / 89: ballots, at any
-  // nranks (85 also in the static tile order)
-  if (tuning_variant() == 83) shape = StagedShape::kOwner8x16;
-  if (tuning_variant() == 87) shape = StagedShape::kOwner4x16;
-  if (tuning_variant() == 85 || tuning_variant() == 89) shape = StagedShape::kBallot4x16;
-#endif
+  const StagedShape shape = hook_staged_shape(staged_shape<Out>(keysize, nranks));
   const u64 st_tile = shape == StagedShape::kOwner8x16 ? 8192 : kStTile;
   const int waves = nranks <= 4096 ? 8 : 4;  // generic: W x nranks x 4 B of LDS <= 128 KiB
   const u64 tile = kind == BucketKernel::kTwoPass ? kTpCountTile
@@ -307,34 +454,15 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
                                                    : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
-  BucketArgs a{};
-  a.k = static_cast<const uint8_t *>(keys);
-  a.n = n;
-  a.rk = make_fastmod(nranks);
-  a.nranks = nranks;
-  while ((1u << a.nbits) < nranks) ++a.nbits;
   a.ts = TileStarts{w.counts, w.chunks, w.base, nranks};
   a.ntiles = ntiles;
-  const size_t hist_lds = (size_t)nranks * 4;
   TwoPass tp{};
-  if (kind == BucketKernel::kTwoPass) {
-    // rank = c * F + f.  Array outputs of 8/16-B keys take one fine bit more
-    // than the balanced split (8192 ranks: F = 256, C = 32): pass 2 writes
-    // 24 / 32 B per key in runs of ~4096 / C keys against pass 1's 12 / 20 B
-    // in runs of ~4096 / F, so longer pass-2 runs pay.  Three boxes, 16M keys
-    // (profiles/r03/ab/bucket_two_pass_digits.log): 8 B at 8192 ranks -5.5 /
-    // 0 / -3.6 %, 16 B at 4096 ranks -4.3 / -4.0 %, 2048 ranks within +-2 %.
-    // 32-B keys (pass 1 writes 36 B/key) lose 3 % with it, and records (AoS
-    // rows, pass-2 runs already >= 1 KiB) 1 %: both keep the balanced split.
-    tp.fbits = (a.nbits + 1) / 2;
-    bool fine_plus = std::is_same<Out, OutSoA>::value && keysize <= 16;
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 164) fine_plus = false;  // the balanced split (r02-r03)
-#endif
-    if (fine_plus && tp.fbits + 1 <= std::min<u32>(8, a.nbits)) ++tp.fbits;
-    tp.F = 1u << tp.fbits;
-    tp.C = (nranks + tp.F - 1) >> tp.fbits;
-    tp.cbits = a.nbits - tp.fbits;
+  if (kind == BucketKernel::kTwoPass) {  // the r02-r05 two-pass form (A/B build only)
+    const Digits d = digit_split<Out>(a.nbits, nranks, keysize);
+    tp.fbits = d.fbits;
+    tp.F = d.F;
+    tp.C = d.C;
+    tp.cbits = d.cbits;
     static_assert(kBucketMaxRanks <= kTpMaxDigits * kTpMaxDigits, "two digits of <= 256 cover every rank");
     if (tp.F > kTpMaxDigits || tp.C > kTpMaxDigits)  // the kernels' LDS digit tables
       return fail("two-pass digit split: a digit of %s%lld buckets exceeds the LDS tables", "",
@@ -349,33 +477,13 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
     tp.iidx = w.iidx;
     tp.ntiles = ntiles;
     tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
-    tp.SG = std::max<u64>(1, (u64)tp.F * kTpSegKeys / ((u64)kTpChunkTiles * kTpCountTile));  // ~kTpSegKeys keys
-    // Segments per fine bucket: the count-chunks are split evenly.  When the
-    // remainder of nchunks / SG leaves at most one extra chunk per segment,
-    // take the floor (segments of SG or SG + 1 chunks: ~3968 keys at most,
-    // spilling ~2 % of the time) rather than the ceiling, whose segments
-    // are ~6 % shorter in the mean but one more per fine bucket -- one more
-    // pass through the sub-tile's phase chain (16M keys at 8192 ranks: 17
-    // segments of 30-31 chunks instead of 18).  Interleaved against the
-    // ceiling, both split evenly (profiles/r05/ab/bucket_pass2_even_segments.log):
-    // 8-B records at 8192 ranks -1.8 % (two 2048-key sub-tiles per segment
-    // either way, 34 sub-tiles per fine bucket instead of 36), arrays within
-    // +-0.5 %.  PDHT_TP_EVEN_SEG=0 (experiment builds): the ceiling.
-    // (only where SG + 1 chunks stay ~2 sigma under 4096 keys: F = 256; at
-    // F <= 128 one chunk more is 256+ keys and would spill half the time)
-    const u64 nfl = std::max<u64>(1, tp.nchunks / tp.SG);
-    const u64 step = (u64)kTpChunkTiles * kTpCountTile / tp.F;  // keys of one fine bucket per chunk
-    const bool floor_ok = PDHT_TP_EVEN_SEG && (tp.SG + 1) * step <= 3968 && tp.nchunks - nfl * tp.SG <= nfl;
-    tp.nsegf = floor_ok ? nfl : (tp.nchunks + tp.SG - 1) / tp.SG;
+    split_segments(tp.nchunks, (u64)kTpChunkTiles * kTpCountTile, tp.F, &tp.SG, &tp.nsegf);
     tp.nseg = (u64)tp.F * tp.nsegf;
   }
   if (ntiles && kind == BucketKernel::kTwoPass) {
     // the count kernel scans the fine counts down each count-chunk itself
-    // (no column-scan launch); tuning 264: the r02-r05 colscan over 32-tile chunks
-    bool fscan = true;
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 264) fscan = false;
-#endif
+    // (no column-scan launch); A/B 264: the r02-r05 colscan over 32-tile chunks
+    const bool fscan = hook_fscan(true);
     tp.fchunk = fscan ? kTpChunkTiles : kBucketChunk;
     const u64 nfchunks = (ntiles + tp.fchunk - 1) / tp.fchunk;
     u32 *cF = fscan ? w.chunksF : nullptr;
@@ -417,15 +525,10 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
                                             kind == BucketKernel::kTwoPass ? w.fbase : nullptr, w.tickets);
   g_kernel = "k_bucket_base";
   if (ntiles) {
-    int rc = 0;
-#ifdef PDHT_HIP_TUNING
-    if (kind == BucketKernel::kStaged && tuning_variant() == 85)  // static tile order (r02 default before)
-      rc = keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
-           : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
-                           : launch_staged<32, Out>(a, out, st, dev);
-    else
-#endif
-    if (kind == BucketKernel::kTwoPass)
+    int rc = hook_staged_launch(kind == BucketKernel::kStaged, keysize, a, out, st, dev);
+    if (rc != kNoVariant) {
+      // an A/B alternative ran
+    } else if (kind == BucketKernel::kTwoPass)
       rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev)
            : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev)
                            : launch_two_pass_sel<32, Out>(a, tp, out, st, dev);
@@ -452,9 +555,15 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
 
 using namespace pdht;
 
-
+// Workspace sizes: array outputs (pdht_bucket_batch_dev) and wire records
+// (pdht_bucket_records_dev) switch to the two-pass sort at different rank
+// counts (32-B records from 1025 ranks, 32-B arrays from 2049), so each has
+// its own query; the records one is never smaller.
 PDHT_API size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks) {
-  return bucket_layout(nullptr, n, keysize, nranks).bytes;
+  return bucket_layout(nullptr, n, keysize, nranks, false).bytes;
+}
+PDHT_API size_t pdht_bucket_records_workspace_bytes(size_t n, size_t keysize, uint32_t nranks) {
+  return bucket_layout(nullptr, n, keysize, nranks, true).bytes;
 }
 
 PDHT_API int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n, uint32_t nptes,
@@ -479,11 +588,10 @@ PDHT_API int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n,
   if ((uintptr_t)records & 7) return fail("records must be 8-byte aligned%s", "");
   const OutRec out{static_cast<uint8_t *>(records), (u64)pdht_bucket_record_bytes(keysize),
                    (u64)msg_type | ((u64)src_rank << 32), ht_index, (u32)keysize};
-#ifdef PDHT_HIP_TUNING
-  if (tuning_variant() == 112) {  // r02 store order: header halves first, {mbits, key} halves a round later
-    const OutRecT<false> o2{out.rec, out.stride, out.hdr, out.ht_index, out.L};
-    return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, o2, 0, bucket_offsets, ST(s));
-  }
-#endif
+  if (int rc = hook_records(out, [&](const auto &o2) {
+        return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, o2, 0, bucket_offsets, ST(s));
+      });
+      rc != kNoVariant)
+    return rc;
   return bucket_impl(keys, keysize, n, nranks, workspace, workspace_bytes, out, 0, bucket_offsets, ST(s));
 }

@@ -1,6 +1,7 @@
 // pdht_fixed128.hip -- device-resident CityHash128 / CityHashCrc128 batches of
 // fixed-length keys (include/pdht_hip.h).
 #include "launch.h"
+#include "pdht_hooks_entry.h"  // A/B hook points (product/: none taken)
 
 using namespace pdht;
 
@@ -21,12 +22,7 @@ PDHT_API int pdht_citycrc128_batch_dev(const void *keys, size_t stride, size_t k
                                        uint64_t *out, pdht_hip_stream_t s) {
   if (n && !out) return fail("null out%s", "");
   if (keylen > 900) {  // CityHashCrc256 rounds: CRC-32C byte tables in LDS
-#ifdef PDHT_HIP_TUNING
-    if (tuning_variant() == 153)  // timing only: no CRC lookups (wrong digests)
-      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 0>{}, Sink128{nullptr, out}, ST(s));
-    if (tuning_variant() == 150)  // r02's 6-bit-slice tables
-      return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 6>{}, Sink128{nullptr, out}, ST(s));
-#endif
+    if (int rc = hook_crc128_long(keys, stride, keylen, n, out, s); rc != kNoVariant) return rc;
     return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128>{}, Sink128{nullptr, out}, ST(s));
   }
   return launch_fixed(keys, stride, keylen, n, AlgoCrc128{}, Sink128{nullptr, out}, ST(s));

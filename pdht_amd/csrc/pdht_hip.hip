@@ -18,12 +18,6 @@ int fail(const char *fmt, const char *a, long long b) {
   return PDHT_HIP_ERROR;
 }
 
-#ifdef PDHT_HIP_TUNING
-static std::atomic<int> g_variant{0};
-static std::atomic<int> g_per_cu{0};
-int tuning_variant() { return g_variant.load(std::memory_order_relaxed); }
-#endif
-
 // ------------------------------------------------------- device state ---
 DevInfo g_dev[kMaxDev];
 
@@ -39,9 +33,7 @@ int current_device(int *dev) {
 }
 
 unsigned grid_for(u64 work_blocks, int per_cu, int dev) {
-#ifdef PDHT_HIP_TUNING
-  if (const int o = g_per_cu.load(std::memory_order_relaxed)) per_cu = o;
-#endif
+  per_cu = hook_per_cu(per_cu);
   const u64 cap = (u64)std::max(1, g_dev[dev].cus) * per_cu;
   return (unsigned)std::max<u64>(1, std::min<u64>(work_blocks, cap));
 }
@@ -92,14 +84,10 @@ int check_place(size_t n, const u64 *mbits, u32 nptes, u32 nranks, const void *r
 using namespace pdht;
 
 // ===================================================================== ABI ===
-static_assert(PDHT_HIP_ABI_VERSION == 3, "bump the version string with the ABI");
-PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.3 (abi 3, gfx950, CityHash v1.0.x)"; }
+static_assert(PDHT_HIP_ABI_VERSION == 4, "bump the version string with the ABI");
+PDHT_API const char *pdht_hip_version(void) { return "pdht-hip 0.4 (abi 4, gfx950, CityHash v1.0.x)"; }
 PDHT_API const char *pdht_hip_last_error(void) { return g_err; }
 PDHT_API const char *pdht_hip_last_kernel(void) { return g_kernel; }
-#ifdef PDHT_HIP_TUNING
-PDHT_API int pdht_hip_set_variant(int v) { return g_variant.exchange(v); }
-PDHT_API int pdht_hip_set_blocks_per_cu(int per_cu) { return g_per_cu.exchange(per_cu); }
-#endif
 
 PDHT_API int pdht_hip_device_count(int *count) {
   if (!count) return fail("null count%s", "");

@@ -1,7 +1,8 @@
 /*
  * pdht_hip_tuning.h -- extra entry points of the TUNING build only
- * (pdht_amd/lib/libpdht_hip_tuning.so, compiled with -DPDHT_HIP_TUNING from
- * the same sources as the product).  Used by tools/ and the A/B tests; not
+ * (pdht_amd/lib/libpdht_hip_tuning.so: the same sources as the product,
+ * compiled with the A/B hook headers of pdht_amd/csrc/tuning/ instead of
+ * pdht_amd/csrc/product/, plus tuning/pdht_tuning.hip).  Used by tools/ and the A/B tests; not
  * part of the drop-in boundary (include/), and not exported by the product
  * library libpdht_hip.so.
  */
@@ -13,9 +14,9 @@ extern "C" {
 #endif
 
 /* Select an alternative kernel where one exists (0 = the product's choice).
- * The alternatives live in pdht_amd/csrc/tuning/ (kernels_tuning.h,
- * launch_tuning.h) and the tuning hooks of the C-ABI sources; the product
- * headers hold only what ships.  Every variant the sources know (DESIGN.md
+ * The alternatives live in pdht_amd/csrc/tuning/ (kernels_tuning.h and the
+ * pdht_hooks*.h headers the sources' hook points resolve to in this build);
+ * the product sources and headers hold only what ships.  Every variant the sources know (DESIGN.md
  * §4 has the measurements):
  *   64-B keys      7  one tile of prefetch per wave, 4 WG/CU (r01: 2-5 % slower)
  *                 26  plain instead of non-temporal digest stores (2-6 % slower)
@@ -79,6 +80,18 @@ extern "C" {
  *                     pass 2 8x4@2 (product: 32-B arrays 267, 16/32-B records 268)
  *                270  16/32-B keys' two passes as r04-r05 shipped them (spilling)
  *            271/272  8-B records' pass 2 in 4x4@4 / 4x8@4 (r04-r05; product 8x4@2)
+ *                290  the r02-r05 two-pass form (counting kernel + fine-count scans
+ *                     ahead of pass 1, pass 1 writing global fine-bucket runs) instead
+ *                     of the tile-local one (r06); 202 and 264-272 imply it
+ *            291-293  tile-local two passes: pass 2 in 4x8@4 / 8x4@2; pass 1 in
+ *                     16x4@1 (4096-key tiles, 1024 threads) (8/16-B keys)
+ *            294/295  tile-local pass 1 on 8192-key tiles (16x8@1), pass-2 gathers of
+ *                     runs twice as long (8/16-B keys); 295 on the balanced digit split
+ *                298  timing probe: tile-local pass 2 reading contiguous rows instead of
+ *                     gathering its f-runs (wrong outputs; 8/16-B keys)
+ *            296/297  tile-local pass-2 segments in chunk-range-major order (the
+ *                     workgroups of an XCD gather neighbouring f-runs of the same tiles);
+ *                     297 with 294's 8192-key tiles
  *                164  two-pass arrays of 8/16-B keys on the balanced digit split
  *                     F = 2^ceil(nbits/2) (product: one fine bit more)
  *   records      112  r02 store order (header halves a staging round early)

@@ -71,11 +71,9 @@ static int zero_copy_run(int device, Launch launch) {
   (void)hipSetDevice(prev);
   return rc;
 }
-#ifdef PDHT_HIP_TUNING
-static bool zero_copy_allowed() { return tuning_variant() != 61; }  // 61: chunked copies (A/B)
-#else
-static constexpr bool zero_copy_allowed() { return true; }
-#endif
+// pinned buffers take the zero-copy path (the A/B build can force the chunked
+// copy pipeline onto them instead)
+static bool zero_copy_allowed() { return hook_zero_copy(true); }
 
 static int slot_reserve(Slot &s, size_t in_bytes, size_t out_bytes) {
   if (!s.st) HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));

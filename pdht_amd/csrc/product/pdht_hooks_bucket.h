@@ -1,0 +1,25 @@
+// product/pdht_hooks_bucket.h -- pdht_bucket.hip's hook points, product
+// build: every choice stays the product's (product/pdht_hooks.h explains the
+// mechanism).
+#pragma once
+
+namespace pdht {
+
+template <class K>
+static inline K hook_bucket_kind(K dflt, bool, u32) { return dflt; }
+template <class S>
+static inline S hook_staged_shape(S dflt) { return dflt; }
+static inline bool hook_fine_plus(bool dflt) { return dflt; }
+static inline bool hook_fscan(bool dflt) { return dflt; }
+static inline bool hook_tile_local(bool dflt) { return dflt; }
+static inline bool hook_tl_sgmajor(bool dflt) { return dflt; }
+template <int L, class Out, class... A>
+static inline int hook_two_pass_shape(A &&...) { return kNoVariant; }
+template <int L, class Out, class... A>
+static inline int hook_tl_shape(A &&...) { return kNoVariant; }
+template <class... A>
+static inline int hook_staged_launch(A &&...) { return kNoVariant; }
+template <class... A>
+static inline int hook_records(A &&...) { return kNoVariant; }
+
+}  // namespace pdht

@@ -32,14 +32,15 @@ int fail(const char *fmt, const char *a = "", long long b = 0);
     if (e_ != hipSuccess) return fail("%s (" #expr ")", hipGetErrorString(e_)); \
   } while (0)
 
-// Tuning build (libpdht_hip_tuning.so, -DPDHT_HIP_TUNING; tools/ and the
-// A/B tests only): a process-wide variant number selects an alternative
-// kernel where one exists, and the workgroups per CU can be overridden.  The
-// product library has neither: one measured-best kernel per path, no
-// process-global mutable state, no environment knobs.
-#ifdef PDHT_HIP_TUNING
-int tuning_variant();
-#endif
+}  // namespace pdht
+
+// A/B hook points (product/pdht_hooks.h: in the product libraries every hook
+// is "not taken" -- one measured-best kernel per path, no process-global
+// mutable state, no environment knobs; tuning/pdht_hooks.h in
+// libpdht_hip_tuning.so, for tools/ and the A/B tests).
+#include "pdht_hooks.h"
+
+namespace pdht {
 
 // ------------------------------------------------------- device state ---
 constexpr int kMaxDev = 64;

@@ -1,0 +1,124 @@
+// tuning/pdht_hooks_bucket.h -- the TUNING build's alternatives of the
+// bucketing choices (pdht_bucket.hip includes "pdht_hooks_bucket.h" after its
+// launch templates; product/pdht_hooks_bucket.h takes none of these).  Every
+// variant was measured against the product form (EXPERIMENTS.md).
+#pragma once
+
+namespace pdht {
+
+// The r02-r05 two-pass form (counting kernel + fine counts scanned ahead of
+// pass 1, pass 1 writing global fine-bucket runs) instead of the tile-local
+// one (r06): 290 as r05 shipped it, and its shape variants below.
+static inline bool tuning_two_pass_r05() {
+  const int v = tuning_variant();
+  return v == 290 || v == 202 || v == 264 || (v >= 265 && v <= 272);
+}
+static inline bool hook_tile_local(bool dflt) { return tuning_two_pass_r05() ? false : dflt; }
+// 296 / 297: tile-local pass-2 segments in chunk-range-major order (the
+// workgroups of an XCD gather neighbouring f-runs of the same tiles at once)
+// / 297 the same and the chunk-range-major order on 8192-key tiles (294)
+static inline bool hook_tl_sgmajor(bool dflt) {
+  return tuning_variant() == 296 || tuning_variant() == 297 ? true : dflt;
+}
+
+// 21: the generic-length kernel for 8/16/32-B keys too; 70: one pass (the
+// staged scatter) up to 2048 ranks whatever the two-pass threshold; 71: two
+// passes at any nranks >= 2.  (r02's gather, producer/consumer and register
+// scatters measured slower than the staged one and were removed in r03.)
+template <class K>
+static inline K hook_bucket_kind(K kind, bool fixed, u32 nranks) {
+  const int v = tuning_variant();
+  if (v == 70 && kind == K::kTwoPass && nranks <= kStagedMaxRanks) kind = K::kStaged;
+  if (v == 71 && fixed && nranks >= 2) kind = K::kTwoPass;
+  if (v == 21) kind = K::kGeneric;
+  return kind;
+}
+
+// 83 / 87: owner ranking on 8 x 16 / 4 x 16 tiles, 85 / 89: ballots, at any
+// nranks (85 also in the static tile order: hook_staged_launch)
+template <class S>
+static inline S hook_staged_shape(S shape) {
+  const int v = tuning_variant();
+  if (v == 83) shape = S::kOwner8x16;
+  if (v == 87) shape = S::kOwner4x16;
+  if (v == 85 || v == 89) shape = S::kBallot4x16;
+  return shape;
+}
+
+// 164: two-pass arrays of 8/16-B keys on the balanced digit split
+static inline bool hook_fine_plus(bool dflt) {
+  return tuning_variant() == 164 || tuning_variant() == 295 ? false : dflt;
+}
+// 264: the r02-r05 fine-count column scan over 32-tile chunks
+static inline bool hook_fscan(bool dflt) { return tuning_variant() == 264 ? false : dflt; }
+
+// Shapes of the r02-r05 two passes.
+template <int L, class Out>
+static int hook_two_pass_shape(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
+  // (r04's shape search, tuning 192-201, removed in r05)
+  constexpr int kW = L == 8 && !Out::kPair8 ? 1 : 0;  // (ONE exists for 8-B arrays only)
+  const int v = tuning_variant();
+  if (v == 202)  // r02-r03: 4 x 8 @ 4 both, pass 2 storing in two phases
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, kTpW, kTpKPL, kTpPerCu, false>(a, tp, out, st, dev);
+  if (kW && v == 265)  // r04-r05 product for 8-B arrays: pass 2 two-phase 4 x 8 @ 4
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2, false>(a, tp, out, st, dev);
+  if (kW && v == 266)  // ONE in 4 x 8 @ 4
+    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+  if constexpr (L >= 16) {  // r05 spill probe (16/32-B keys in 4 keys per lane) and the r04-r05 shapes
+    switch (v) {
+      case 267: return launch_two_pass<L, Out, 8, 4, 2, 8, 4, 2>(a, tp, out, st, dev);
+      case 268: return launch_two_pass<L, Out, 4, 4, 4, 8, 4, 2>(a, tp, out, st, dev);
+      case 269: return launch_two_pass<L, Out, 8, 4, 2, 4, 8, 4>(a, tp, out, st, dev);
+      case 270:
+        if constexpr (L == 16) return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
+        else return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+      default: break;
+    }
+  }
+  if constexpr (L == 8 && Out::kPair8) {  // 8-B records' pass 2: 4 x 4 @ 4 / r04-r05's 4 x 8 @ 4
+    if (v == 271) return launch_two_pass<L, Out, 4, 4, 4, 8, 8, 2>(a, tp, out, st, dev);
+    if (v == 272) return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
+  }
+  return kNoVariant;
+}
+
+// Shapes of the tile-local two passes (r06).  291: pass 2 in 4 x 8 @ 4;
+// 292: pass 2 in 8 x 4 @ 2; 293: pass 1 in 16 x 4 (4096-key tiles, 1024
+// threads) @ 1; 294: pass 1 on 8192-key tiles (16 x 8 @ 1; hook_tl_tile_shift),
+// pass-2 runs twice as long; 295: 294 on the balanced digit split.
+template <int L, class Out>
+static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
+                         uint64_t *bucket_offsets, hipStream_t st, int dev) {
+  const int v = tuning_variant();
+  if constexpr (L <= 16) {
+    if (v == 298)  // timing probe: pass 2 reading contiguous rows (wrong outputs)
+      return launch_tl<L, Out, 8, 8, 2, 8, 8, 2, 1>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 291) return launch_tl<L, Out, 4, 8, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 292) return launch_tl<L, Out, 8, 4, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 293) return launch_tl<L, Out, 8, 8, 2, 16, 4, 1>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 294 || v == 295 || v == 297)
+      return launch_tl<L, Out, 8, 8, 2, 16, 8, 1>(a, tl, out, w, bucket_offsets, st, dev);
+  }
+  return kNoVariant;
+}
+
+// 85: the staged scatter in the static tile order (the r02 default before the
+// per-XCD tickets)
+template <class Out>
+static int hook_staged_launch(bool staged, size_t keysize, const BucketArgs &a, const Out &out, hipStream_t st,
+                              int dev) {
+  if (!staged || tuning_variant() != 85) return kNoVariant;
+  return keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
+         : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
+                         : launch_staged<32, Out>(a, out, st, dev);
+}
+
+// 112: the r02 record store order (header halves first, {mbits, key} halves
+// a round later)
+template <class Go>
+static int hook_records(const OutRec &out, Go &&go) {
+  if (tuning_variant() != 112) return kNoVariant;
+  return go(OutRecT<false>{out.rec, out.stride, out.hdr, out.ht_index, out.L});
+}
+
+}  // namespace pdht

@@ -1,6 +1,7 @@
-// tuning/launch_tuning.h -- the TUNING build's alternative launch shapes of
-// the hash paths (launch.h calls one hook per path, inside #ifdef
-// PDHT_HIP_TUNING; the product library compiles none of this).  A hook
+// tuning/pdht_hooks_launch.h -- the TUNING build's alternative launch shapes
+// of the hash paths: launch.h calls one hook per path, which the product
+// build resolves to product/pdht_hooks_launch.h (none taken) and
+// libpdht_hip_tuning.so to this header (-Ipdht_amd/csrc/tuning).  A hook
 // returns kNoVariant when the process-wide variant (pdht_hip_set_variant)
 // does not concern it, else the launch's status.  Every variant here was
 // measured against the product shape (logs in profiles/):
@@ -22,11 +23,10 @@
 //                digest stores; 203 / 204 s_setprio 3 / 1; 205 no s_setprio;
 //                252 workgroup-combined digest stores (2 KiB runs)
 #pragma once
+#include "pdht_hooks.h"
 #include "kernels_tuning.h"
 
 namespace pdht {
-
-constexpr int kNoVariant = -1;
 
 static int tuning_launched() {
   HIP_TRY(hipGetLastError());
@@ -34,7 +34,7 @@ static int tuning_launched() {
 }
 
 template <class Algo, class Sink>
-static int tuning_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Sink sink, hipStream_t st, int dev,
+static int hook_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Sink sink, hipStream_t st, int dev,
                         u64 blocks) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt snt = NtSink<Sink>::make(sink);
@@ -90,21 +90,21 @@ static int tuning_small(size_t keylen, const uint8_t *k, size_t n, Algo algo, Si
   return kNoVariant;
 }
 
-// launch size (bytes of keys per launch); 0 = the product's
-static u64 tuning_chunk_bytes() {
+// launch size (bytes of keys per launch); dflt = the product's
+static u64 hook_chunk_bytes(u64 dflt) {
   switch (tuning_variant()) {
     case 114: return 256ull << 20;
     case 115: return 1ull << 30;
     case 116: return 2ull << 30;
     case 117: return 4ull << 30;
     case 118: return ~0ull;
-    default: return 0;
+    default: return dflt;
   }
 }
 
 // packed, 16-B aligned 64-B keys
 template <class Algo, class Sink>
-static int tuning_xpose64(const uint8_t *k, size_t n, Algo algo, Sink sink, hipStream_t st, int dev) {
+static int hook_xpose64(const uint8_t *k, size_t n, Algo algo, Sink sink, hipStream_t st, int dev) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt sink_nt = NtSink<Sink>::make(sink);
   switch (tuning_variant()) {
@@ -161,10 +161,11 @@ static int tuning_xpose64(const uint8_t *k, size_t n, Algo algo, Sink sink, hipS
   }
 }
 
-// CRC-table algorithms on keys > 900 B, 16-B aligned rows
+// CRC-table algorithms on keys > 900 B (16-B aligned rows only)
 template <class Algo, class Sink>
-static int tuning_crc_long(const uint8_t *k, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
-                           hipStream_t st, int dev, u64 blocks) {
+static int hook_crc_long(const uint8_t *k, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
+                         hipStream_t st, int dev, u64 blocks) {
+  if (((uintptr_t)k & 15) || stride % 16) return kNoVariant;
   const int v = tuning_variant();
   if (v >= 279 && v <= 281 && stride == keylen && (keylen == 1024 || keylen == 2048 || keylen == 4096)) {
     // the LDS-DMA ring (k_long_ring): R = 4 / 2 / 3 line-rounds per wave
@@ -200,7 +201,7 @@ static int tuning_crc_long(const uint8_t *k, size_t stride, size_t keylen, size_
 
 // fixed keys too long for a 64-key window, 16-B aligned rows
 template <class Algo, class Sink>
-static int tuning_long_walk(const uint8_t *k, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
+static int hook_long_walk(const uint8_t *k, size_t stride, size_t keylen, size_t n, Algo algo, Sink sink,
                             hipStream_t st, int dev, u64 blocks, int per_cu) {
   if (tuning_variant() != 96) return kNoVariant;
   typedef typename NtSink<Sink>::type SinkNt;
@@ -213,7 +214,7 @@ static int tuning_long_walk(const uint8_t *k, size_t stride, size_t keylen, size
 
 // variable-length keys; may also force the window width (12 / 13)
 template <class Algo, class Sink>
-static int tuning_var(const uint8_t *b, const u64 *offsets, u64 obase, size_t n, Algo algo, Sink sink,
+static int hook_var(const uint8_t *b, const u64 *offsets, u64 obase, size_t n, Algo algo, Sink sink,
                       hipStream_t st, int dev, u64 wb, bool &wide) {
   typedef typename NtSink<Sink>::type SinkNt;
   const SinkNt sink_nt = NtSink<Sink>::make(sink);

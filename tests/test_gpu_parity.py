@@ -593,6 +593,16 @@ BUCKET_CASES += [(L, nr, n, 164) for L in (8, 16, 32) for nr in (1025, 2049, 409
                  for n in (4095, 300007, (1 << 20) + 5)]
 # the product's fine-plus split at its edges: 71 forces two passes from 2 ranks (nbits 1..3)
 BUCKET_CASES += [(L, nr, 70001, 71) for L in (8, 32) for nr in (2, 3, 4, 5, 8, 9)]
+# r06 tile-local two passes: count-chunks of ct = 1 / 2 / 4 tiles (ct doubles
+# from 512 chunks up: 2M / 4M / 8M keys), pass-2 segments of SG or SG + 1
+# chunks split evenly (8192 ranks, n ~1.1M / 2.1M keys: ADVICE r05), 1025 and
+# 8192 ranks (F = 64 / 256), ragged last tiles
+BUCKET_CASES += [(L, nr, n, 0) for L in (8, 16) for nr in (8192,) for n in ((1 << 20) + 100_003, (2 << 20) + 100_003)]
+BUCKET_CASES += [(L, nr, n, 0) for L in (8, 32) for nr in (2049, 8192) for n in ((4 << 20) + 7, (8 << 20) + 4097)]
+# 290: the r02-r05 two-pass form (counting kernel ahead of pass 1, global fine-bucket runs);
+# 291-293: tile-local shapes (pass 2 in 4 x 8 @ 4 / 8 x 4 @ 2; pass 1 in 16 x 4 @ 1)
+BUCKET_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293) for L in (8, 16, 32) for nr in (2049, 8192)
+                 for n in (4095, 300007, (1 << 20) + 5)]
 
 
 def _bucket_kernel(L, nranks, variant, records=False):
@@ -610,7 +620,9 @@ def _bucket_kernel(L, nranks, variant, records=False):
         two_pass_from = {8: 1536, 16: 1025, 32: 1025 if records else 2049}[L]
         one_pass = variant == 70 and nranks <= 2048
         if (variant == 71 and nranks >= 2) or (not one_pass and nranks >= two_pass_from):
-            return f"k_bucket_pass2<{L}B>"
+            # the tile-local form (r06); the r02-r05 form under 290 and its shape variants
+            r05 = variant in (290, 202, 264) or 265 <= variant <= 272
+            return f"k_bucket_pass2<{L}B>" if r05 else f"k_bucket_tl_pass2<{L}B>"
         # staged_shape(): owner-table ranking for array outputs from 512
         # ranks, on 8 x 16 tiles for 8/16-B keys while 81920 + 52 B per rank
         # of LDS fits a CU, else on 4 x 16 tiles while 40960 + 28 B per rank
@@ -675,18 +687,20 @@ def test_bucket_skewed(dev, oracle, L, nranks, variant):
     assert (offs.cpu().numpy() == want_offs).all()
 
 
-@pytest.mark.parametrize("L", [8, 16, 13])
-def test_bucket_optional_outputs(dev, oracle, L):
+@pytest.mark.parametrize("L,nranks", [(8, 1000), (16, 1000), (13, 1000), (8, 2049), (16, 2049), (8, 8192),
+                                      (16, 8192)])
+def test_bucket_optional_outputs(dev, oracle, L, nranks):
     """Each of keys_out / ptindex_out / index_out may be omitted (NULL);
-    mbits and the offsets are the same either way."""
+    mbits and the offsets are the same either way -- on the one-pass and on
+    the two-pass path (2049 / 8192 ranks)."""
     rng = np.random.default_rng(L)
     n = 50_000
     k = rng.integers(0, 256, (n, L), dtype=np.uint8)
     kd = to_dev(k, dev)
-    m2, p2, r2 = oracle.pdht_hash_fixed(k, 1, 1000)
+    m2, p2, r2 = oracle.pdht_hash_fixed(k, 1, nranks)
     order = np.argsort(r2, kind="stable")
     for wk, wp, wi in ((False, False, True), (True, False, False), (False, False, False)):
-        ko, mb, pt, ix, offs = P.bucket_batch(kd, 1, 1000, with_keys=wk, with_ptindex=wp, with_index=wi)
+        ko, mb, pt, ix, offs = P.bucket_batch(kd, 1, nranks, with_keys=wk, with_ptindex=wp, with_index=wi)
         assert (ko is not None) == wk and (pt is not None) == wp and (ix is not None) == wi
         assert (u64(mb) == m2[order]).all()
         if ix is not None:
@@ -711,6 +725,10 @@ RECORD_CASES += [(L, nr, n, v) for v in (267, 268, 269, 270) for L in (16, 32) f
 RECORD_CASES += [(8, nr, n, v) for v in (271, 272) for nr in (2049, 8192) for n in (4097, 300007, (1 << 20) + 5)]
 # 112: the r02 store order of 8-B records (header halves a staging round early)
 RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
+# r06: records on the r02-r05 two-pass form (290) and the tile-local shapes 291-293
+RECORD_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293) for L in (8, 16, 32) for nr in (2049, 8192)
+                 for n in (4097, 300007)]
+RECORD_CASES += [(L, 8192, (4 << 20) + 7, 0) for L in (8, 32)]
 
 
 @pytest.mark.parametrize("L,nranks,n,variant", _tuning_marked(RECORD_CASES))

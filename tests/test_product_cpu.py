@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
     want = set()
     for h in ("pdht_hip.h", "pdht_city.h", "pdht_hash.h"):
         want |= _declared(h)
-    assert len(want) == 43, sorted(want)
+    assert len(want) == 44, sorted(want)
     missing = sorted(want - exported)
     assert not missing, missing
     lib = P.lib()
@@ -76,6 +76,25 @@ def test_tuning_entry_points_only_in_tuning_build():
     assert TUNING_SYMS <= _exports(P.TUNING_LIB_PATH)
     src = open(os.path.join(ROOT, "pdht_amd", "csrc", "pdht_hip.hip")).read()
     assert "getenv" not in src
+
+
+def test_product_sources_carry_no_tuning_code():
+    """the A/B alternatives live in pdht_amd/csrc/tuning/
+    and reach the sources only through the "pdht_hooks*.h" headers, which the
+    product build takes from pdht_amd/csrc/product/ (every hook a no-op): no
+    product source or header names the tuning build, its variant state or a
+    tuning header, and every product hook header has a tuning counterpart."""
+    csrc = os.path.join(ROOT, "pdht_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")) and f != "pdht_hip_tuning.h":
+            src = open(os.path.join(csrc, f)).read()
+            for word in ("PDHT_HIP_TUNING", "tuning_variant", "\"tuning/", "kernels_tuning"):
+                assert word not in src, (f, word)
+    prod = sorted(os.listdir(os.path.join(csrc, "product")))
+    assert prod and all(h.startswith("pdht_hooks") for h in prod)
+    assert set(prod) <= set(os.listdir(os.path.join(csrc, "tuning")))
+    for h in prod:
+        assert "tuning_variant" not in open(os.path.join(csrc, "product", h)).read()
 
 
 def test_weakhash_exports(golden):
@@ -231,14 +250,20 @@ def test_bucket_workspace_small_at_low_rank_counts():
     """The two-pass intermediate (n x (keysize + 4) B) is reserved only at
     the rank counts that take the two-pass sort."""
     n = 16 << 20
-    for L, thr in ((8, 1536), (16, 1025), (32, 1025)):  # 32-B: records' threshold (arrays: 2049)
-        small = P.bucket_workspace_bytes(n, L, 1024 if L != 16 else 1000)
+    for records, L, thr in ((False, 8, 1536), (False, 16, 1025), (False, 32, 2049),
+                            (True, 8, 1536), (True, 16, 1025), (True, 32, 1025)):
+        ws = lambda r: P.bucket_workspace_bytes(n, L, r, records=records)  # noqa: E731
+        small = ws(1024 if L != 16 else 1000)
         assert small < 64 << 20, (L, small)
-        assert P.bucket_workspace_bytes(n, L, thr) >= small + n * (L + 4)
-        assert P.bucket_workspace_bytes(n, L, thr - 1) < n * (L + 4)
+        assert ws(thr) >= small + n * (L + 4)  # either two-pass form fits
+        assert ws(thr - 1) < n * (L + 4)
+        assert ws(8192) >= P.bucket_workspace_bytes(n, L, 8192)
+    # ADVICE r05: 32-B array callers at 1025..2048 ranks do not reserve records' intermediate
+    assert P.bucket_workspace_bytes(n, 32, 2048) < n * 36
+    assert P.bucket_workspace_bytes(n, 32, 2048, records=True) >= n * 36
     assert P.bucket_workspace_bytes(n, 8, 7) < 1 << 20
     assert P.bucket_workspace_bytes(n, 13, 8192) < n * 17  # generic lengths never take two passes
-    assert b"abi 3" in P.lib().pdht_hip_version()
+    assert b"abi 4" in P.lib().pdht_hip_version()
 
 
 def test_device_wrappers_reject_cpu_tensors():

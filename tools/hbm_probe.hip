@@ -278,7 +278,167 @@ __global__ __launch_bounds__(256) void wr(u32x4 *__restrict__ p, u64 ntile) {
     }
 }
 
+// cfg3's byte mix with plain coalesced accesses, no LDS and no hash (VERDICT
+// r05 item 3): per 64-key tile a wave reads the tile's u64 offsets (one per
+// lane), the tile's contiguous key bytes in 16-B pieces (every lane folds its
+// pieces), and writes one 8-B digest per lane.
+//   cfg3mix<NT,PERWAVE>  uniform 136-B keys: the key range of tile t is
+//                    [t*8704, (t+1)*8704), independent of the offsets (no
+//                    dependent round trip): the byte mix's own ceiling
+//   cfg3dep<NT>      the real cfg3 offsets: the key range is read from the
+//                    offsets first (offsets -> bytes, one dependent round trip
+//                    per tile, as every offset-indexed kernel must)
+// NT: non-temporal loads and digest stores.  PERWAVE: tiles a wave has in
+// flight (loads of all issued before any is folded).
+template <bool NT, int PERWAVE>
+__global__ __launch_bounds__(256) void cfg3mix(const uint8_t *__restrict__ keys, const u64 *__restrict__ offs,
+                                               u64 ntiles, u64 *__restrict__ dig) {
+  constexpr u32 kTileBytes = 64 * 136;  // 8704 B = 544 pieces of 16 B
+  constexpr int kPieces = kTileBytes / 16, kPer = (kPieces + 63) / 64;
+  const u32 lane = threadIdx.x & 63;
+  const u64 wave = (u64)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const u64 nw = (u64)gridDim.x * 4;
+  for (u64 t0 = wave * PERWAVE; t0 < ntiles; t0 += nw * PERWAVE) {
+    u32x4 v[PERWAVE][kPer];
+    u64 o[PERWAVE];
+#pragma unroll
+    for (int w = 0; w < PERWAVE; ++w) {
+      const u64 t = min(t0 + w, ntiles - 1);
+      o[w] = NT ? __builtin_nontemporal_load(offs + t * 64 + lane) : offs[t * 64 + lane];
+      const u32x4 *q = reinterpret_cast<const u32x4 *>(keys + t * kTileBytes);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int pc = j * 64 + lane;
+        v[w][j] = pc < kPieces ? ld<NT>(q + pc) : u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < PERWAVE; ++w) {
+      if (t0 + w >= ntiles) break;
+      u32x4 f = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) f ^= v[w][j] * (u32)(2 * j + 1);
+      const u64 h = (((u64)(f.x ^ f.z) << 32) | (f.y ^ f.w)) ^ o[w];
+      if (NT) __builtin_nontemporal_store(h, dig + (t0 + w) * 64 + lane);
+      else dig[(t0 + w) * 64 + lane] = h;
+    }
+  }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void cfg3dep(const uint8_t *__restrict__ keys, const u64 *__restrict__ offs,
+                                               u64 n, u64 *__restrict__ dig) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 wave = (u64)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const u64 nw = (u64)gridDim.x * 4;
+  const u64 ntiles = (n + 63) / 64;
+  for (u64 t = wave; t < ntiles; t += nw) {
+    const u64 k = min(t * 64 + lane, n - 1);
+    const u64 o = NT ? __builtin_nontemporal_load(offs + k) : offs[k];
+    const u64 hi_k = min(t * 64 + 64, n);
+    const u64 end = __shfl(NT ? __builtin_nontemporal_load(offs + hi_k) : offs[hi_k], 0);
+    const u64 beg = __shfl(o, 0);
+    const u64 a0 = beg & ~15ull, a1 = (end + 15) & ~15ull;
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(keys + a0);
+    const u64 np = (a1 - a0) / 16;
+    u32x4 f = {0, 0, 0, 0};
+    for (u64 j0 = 0; j0 < np; j0 += 64 * 8) {
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const u64 pc = j0 + j * 64 + lane;
+        v[j] = pc < np ? ld<NT>(q + pc) : u32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f ^= v[j] * (u32)(2 * j + 1);
+    }
+    const u64 h = (((u64)(f.x ^ f.z) << 32) | (f.y ^ f.w)) ^ o;
+    if (t * 64 + lane < n) {
+      if (NT) __builtin_nontemporal_store(h, dig + t * 64 + lane);
+      else dig[t * 64 + lane] = h;
+    }
+  }
+}
+
+static u64 splitmix64_at(u64 seed, u64 k) {
+  u64 z = seed + (k + 1) * 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
 int main(int argc, char **argv) {
+  const char *set0 = getenv("PROBE_SET");
+  if (set0 && std::string(set0) == "cfg3") {
+    // cfg3: 64M keys of 16..256 B (bench.py mixed_lengths: 16 + splitmix64(SEED_LENS, i) % 241),
+    // offsets[n+1], digests[n]; and the uniform 136-B form of the same byte mix
+    const u64 n = 64ull << 20;
+    std::vector<u64> hoff(n + 1);
+    hoff[0] = 0;
+    for (u64 i = 0; i < n; ++i) hoff[i + 1] = hoff[i] + 16 + splitmix64_at(0x1E575EED1E575EEDull, i) % 241;
+    const u64 total = hoff[n], uni = n * 136;
+    const u64 kbytes = std::max(total, uni) + 4096;
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    uint8_t *keys;
+    u64 *offs, *uoffs, *dig;
+    CK(hipMalloc(&keys, kbytes));
+    CK(hipMalloc(&offs, (n + 1) * 8));
+    CK(hipMalloc(&uoffs, (n + 1) * 8));
+    CK(hipMalloc(&dig, n * 8));
+    CK(hipMemset(keys, 0x5a, kbytes));
+    CK(hipMemcpy(offs, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    for (u64 i = 0; i <= n; ++i) hoff[i] = i * 136;
+    CK(hipMemcpy(uoffs, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    CK(hipDeviceSynchronize());
+    const double real_b = (double)total + 16.0 * n + 8, uni_b = (double)uni + 16.0 * n + 8;
+    struct C3 {
+      std::string name;
+      int pc;
+      double bytes;
+      std::function<void(unsigned)> go;
+      std::vector<float> ms;
+    };
+    std::vector<C3> cs;
+    const u64 ntiles = n / 64;
+    for (int pc : {2, 4, 8}) {
+      cs.push_back({"cfg3dep<nt>", pc, real_b, [=](unsigned g) { cfg3dep<true><<<g, 256>>>(keys, offs, n, dig); }, {}});
+      cs.push_back({"cfg3dep<plain>", pc, real_b, [=](unsigned g) { cfg3dep<false><<<g, 256>>>(keys, offs, n, dig); }, {}});
+      cs.push_back({"cfg3mix<nt,1>", pc, uni_b, [=](unsigned g) { cfg3mix<true, 1><<<g, 256>>>(keys, uoffs, ntiles, dig); }, {}});
+      cs.push_back({"cfg3mix<plain,1>", pc, uni_b, [=](unsigned g) { cfg3mix<false, 1><<<g, 256>>>(keys, uoffs, ntiles, dig); }, {}});
+    }
+    for (int pc : {2, 4}) {
+      cs.push_back({"cfg3mix<nt,2>", pc, uni_b, [=](unsigned g) { cfg3mix<true, 2><<<g, 256>>>(keys, uoffs, ntiles, dig); }, {}});
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto &c : cs) c.go(cus * c.pc);
+    CK(hipDeviceSynchronize());
+    CK(hipGetLastError());
+    const int reps = argc > 2 ? atoi(argv[2]) : 10;
+    for (int r = 0; r < reps; ++r)
+      for (auto &c : cs) {
+        CK(hipEventRecord(e0));
+        c.go(cus * c.pc);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        c.ms.push_back(ms);
+      }
+    CK(hipGetLastError());
+    printf("{\"cfg3_key_bytes\": %llu, \"uniform_key_bytes\": %llu, \"keys\": %llu}\n", (unsigned long long)total,
+           (unsigned long long)uni, (unsigned long long)n);
+    for (auto &c : cs) {
+      std::vector<float> v = c.ms;
+      std::sort(v.begin(), v.end());
+      const float med = v[v.size() / 2];
+      printf("{\"case\": \"%s\", \"per_cu\": %d, \"median_ms\": %.4f, \"min_ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n",
+             c.name.c_str(), c.pc, med, v[0], c.bytes / med / 1e6, c.bytes / med / 1e6 / 8000.0);
+    }
+    return 0;
+  }
   const double gib = argc > 1 ? atof(argv[1]) : 1.0;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
   const u64 bytes = (u64)(gib * (1ull << 30)) & ~4095ull;
