@@ -42,12 +42,14 @@ static u32 two_pass_min_ranks(size_t keysize, bool records) {
   return keysize == 8 ? 1536 : keysize == 16 ? 1025 : records ? 1025 : 2049;
 }
 // Tile-local two-pass sort (r06, bucket.h k_bucket_tl_*): pass-1 tiles of
-// 4096 keys (2048 for 32-B keys: 8 waves x 4 keys per lane, spill-free), one
+// 4096 keys for 8-B keys, 2048 for 16/32-B keys (8 waves x 4 keys per lane,
+// spill-free; 16-B keys in 4096-key tiles spilled 23 VGPRs and ran 0.4-1.9 %
+// slower, profiles/r06/ab/bucket_16_tl_pass1_tiles.log), one
 // sub-tile each; count-chunks of ct tiles, ct the largest power of two <= 8
 // that still leaves >= 512 chunks (two pass-1 workgroups on each of 256
 // CUs), so that a chunk's histogram never counts past 32768 keys (u16 halves
 // in LDS).  Both depend on n only, so the workspace size does too.
-static u32 tl_tile_shift(size_t keysize) { return hook_tl_tile_shift(keysize == 32 ? 11 : 12, keysize); }
+static u32 tl_tile_shift(size_t keysize) { return hook_tl_tile_shift(keysize == 8 ? 12 : 11, keysize); }
 static u32 tl_chunk_tiles(u64 ntiles, u32 tshift) {
   u32 ct = std::min<u32>(8, 32768u >> tshift);
   while (ct > 1 && ntiles / ct < 512) ct >>= 1;
@@ -276,7 +278,7 @@ static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out
 }
 
 // Tile-local shapes: pass 1 one tile per sub-tile (8 waves x 8 keys per
-// lane = 4096 keys; 32-B keys 8 x 4 = 2048, spill-free) at 2 WG/CU; pass 2
+// lane = 4096 keys; 16/32-B keys 8 x 4 = 2048, spill-free) at 2 WG/CU; pass 2
 // the shapes the r02-r05 pass 2 measured best per key size and output kind
 // (launch_two_pass_sel).
 template <int L, class Out>
@@ -288,8 +290,10 @@ static int launch_tl_sel(const BucketArgs &a, const TwoPassTL &tl, const Out &ou
   else if constexpr (L == 32)
     return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
   else if constexpr (L == 16 && Out::kPair8)
-    return launch_tl<L, Out, 4, 4, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
-  else if constexpr (L == 16 || (L == 8 && !Out::kPair8))
+    return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 16)
+    return launch_tl<L, Out, 8, 8, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 8 && !Out::kPair8)
     return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
   else
     return launch_tl<L, Out, 8, 4, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
@@ -325,12 +329,15 @@ static Digits digit_split(u32 nbits, u32 nranks, size_t keysize) {
 // (segments of SG or SG + 1 chunks: ~3968 keys at most) rather than the
 // ceiling, whose segments are ~6 % shorter in the mean but one more per fine
 // bucket -- one more pass through the sub-tile's phase chain (16M keys at
-// 8192 ranks: 17 segments of 30-31 chunks instead of 18).  Interleaved
-// against the ceiling (profiles/r05/ab/bucket_pass2_even_segments.log):
-// 8-B records at 8192 ranks -1.8 %, arrays within +-0.5 %.  PDHT_TP_EVEN_SEG=0
-// (experiment builds): the ceiling.  (Only where SG + 1 chunks stay ~2 sigma
-// under 4096 keys: at F <= 128 one chunk more is 256+ keys and would spill
-// half the time.)
+// 8192 ranks: 17 segments of 30-31 chunks instead of 18).  The even split
+// measured equal to a short tail segment for arrays (+-0.5 %,
+// profiles/r05/ab/bucket_pass2_even_segments.log; the -1.8 % that log shows
+// for 8-B records came from their even split alone: records use the balanced
+// digits, F = 128 at 8192 ranks, so they always take the ceiling).  The
+// floor applies only where SG + 1 chunks stay ~2 sigma under 4096 keys: F =
+// 256 (one chunk more at F <= 128 is 256+ keys and would spill a segment into
+// a second sub-tile half the time).  PDHT_TP_EVEN_SEG=0 (experiment builds):
+// the ceiling.
 static void split_segments(u64 nchunks, u64 chunk_keys, u32 F, u64 *SG, u64 *nsegf) {
   *SG = std::max<u64>(1, (u64)F * kTpSegKeys / chunk_keys);
   const u64 nfl = std::max<u64>(1, nchunks / *SG);

@@ -89,6 +89,8 @@ extern "C" {
  *                     runs twice as long (8/16-B keys); 295 on the balanced digit split
  *                298  timing probe: tile-local pass 2 reading contiguous rows instead of
  *                     gathering its f-runs (wrong outputs; 8/16-B keys)
+ *                302  tile-local, 16-B keys: pass 1 in 8x8 (4096-key tiles; spills 23 VGPRs,
+ *                     0.4-1.9 % slower than the product's 8x4)
  *            296/297  tile-local pass-2 segments in chunk-range-major order (the
  *                     workgroups of an XCD gather neighbouring f-runs of the same tiles);
  *                     297 with 294's 8192-key tiles

@@ -28,6 +28,7 @@ static inline bool hook_bucket_reserve(bool, size_t keysize) {
 // 294 / 295: tile-local pass-1 tiles of 8192 keys (8/16-B keys)
 static inline unsigned hook_tl_tile_shift(unsigned dflt, size_t keysize) {
   const int v = tuning_variant();
+  if (v == 302 && keysize == 16) return 12;  // 16-B keys' pass 1 in 4096-key tiles (8 x 8, r06 first form)
   return (v == 294 || v == 295 || v == 297) && keysize <= 16 ? 13 : dflt;
 }
 

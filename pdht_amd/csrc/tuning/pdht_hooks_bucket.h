@@ -91,6 +91,13 @@ static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &ou
                          uint64_t *bucket_offsets, hipStream_t st, int dev) {
   const int v = tuning_variant();
   if constexpr (L <= 16) {
+    if constexpr (L == 16)
+      if (v == 302) {  // pass 1 in 8 x 8 (4096-key tiles, hook_tl_tile_shift), pass 2 as the product's
+        if constexpr (Out::kPair8)
+          return launch_tl<L, Out, 4, 4, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+        else
+          return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+      }
     if (v == 298)  // timing probe: pass 2 reading contiguous rows (wrong outputs)
       return launch_tl<L, Out, 8, 8, 2, 8, 8, 2, 1>(a, tl, out, w, bucket_offsets, st, dev);
     if (v == 291) return launch_tl<L, Out, 4, 8, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
