@@ -29,9 +29,9 @@ HOOKS_TUNING  := -Ipdht_amd/csrc/tuning
 CFLAGS_SHIM = -std=c99 -O3 -fPIC -fvisibility=hidden -Wall -Wextra -Iinclude
 
 HIP_HDR := pdht_amd/csrc/city_core.h pdht_amd/csrc/kernels.h pdht_amd/csrc/runtime.h \
-           pdht_amd/csrc/bucket.h pdht_amd/csrc/launch.h \
-           $(wildcard pdht_amd/csrc/product/*.h) $(wildcard pdht_amd/csrc/tuning/*.h) \
-           pdht_amd/csrc/pdht_hip_tuning.h include/pdht_hip.h include/pdht_city.h
+           pdht_amd/csrc/bucket.h pdht_amd/csrc/launch.h include/pdht_hip.h include/pdht_city.h
+HDR_PRODUCT := $(wildcard pdht_amd/csrc/product/*.h)
+HDR_TUNING := $(wildcard pdht_amd/csrc/tuning/*.h) pdht_amd/csrc/pdht_hip_tuning.h
 SHIM_HDR := include/pdht_hash.h include/pdht_hip.h include/pdht_city.h
 # the C-ABI in translation units that build in parallel (make -j)
 HIP_UNITS := pdht_hip pdht_fixed64 pdht_fixed128 pdht_var pdht_host pdht_bucket
@@ -58,19 +58,20 @@ product: $(LIB) $(LIB_MPI) $(LIB_TUN)
 $(LIBDIR)/pdht_bucket.o $(LIBDIR)/pdht_bucket.tun.o: pdht_amd/csrc/bucket.h
 $(foreach u,pdht_fixed64 pdht_fixed128 pdht_var pdht_host,$(LIBDIR)/$(u).o $(LIBDIR)/$(u).tun.o): pdht_amd/csrc/launch.h
 
-$(LIBDIR)/%.o: pdht_amd/csrc/%.hip $(HIP_HDR)
+# (product objects never see the tuning headers, and the reverse)
+$(LIBDIR)/%.o: pdht_amd/csrc/%.hip $(HIP_HDR) $(HDR_PRODUCT)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) $(HOOKS_PRODUCT) -c -o $@ $<
 
-$(LIBDIR)/%.tun.o: pdht_amd/csrc/%.hip $(HIP_HDR)
+$(LIBDIR)/%.tun.o: pdht_amd/csrc/%.hip $(HIP_HDR) $(HDR_TUNING)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) $(HOOKS_TUNING) -c -o $@ $<
 
-$(LIBDIR)/pdht_tuning.tun.o: pdht_amd/csrc/tuning/pdht_tuning.hip $(HIP_HDR)
+$(LIBDIR)/pdht_tuning.tun.o: pdht_amd/csrc/tuning/pdht_tuning.hip $(HIP_HDR) $(HDR_TUNING)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) $(HOOKS_TUNING) -c -o $@ $<
 
-$(LIBDIR)/%.exp.o: pdht_amd/csrc/%.hip $(HIP_HDR) FORCE
+$(LIBDIR)/%.exp.o: pdht_amd/csrc/%.hip $(HIP_HDR) $(HDR_TUNING) FORCE
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) $(HOOKS_TUNING) $(EXP) -c -o $@ $<
 

@@ -28,6 +28,7 @@ extern "C" {
  *   long keys     96  r02 spans before the 128-B line spans (240-B / 64-B)
  *                153  timing only: CRC lookups replaced by a fold (wrong digests)
  *                150  CRC-32C on r02's 6-bit-slice tables (product: byte tables)
+ *                303  CRC-32C on 11-bit-slice tables (6 lookups per word, 42 KiB)
  *            279-281  CRC long keys of 1024 / 2048 / 4096 B through an LDS-DMA ring of
  *                     R = 4 / 2 / 3 coalesced line-rounds per wave (k_long_ring)
  *            190/191  CityHashCrc256Long's block loop as a 128-B line stream

@@ -151,6 +151,8 @@ static int hook_crc128_long(const void *keys, size_t stride, size_t keylen, size
     return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 0>{}, Sink128{nullptr, out}, ST(s));
   if (tuning_variant() == 150)  // r02's 6-bit-slice tables
     return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 6>{}, Sink128{nullptr, out}, ST(s));
+  if (tuning_variant() == 303)  // r06: 11-bit-slice tables (6 lookups per word)
+    return launch_fixed(keys, stride, keylen, n, CrcLds<AlgoCrc128, 11>{}, Sink128{nullptr, out}, ST(s));
   return kNoVariant;
 }
 

@@ -134,10 +134,10 @@ def test_crc128_long_keys_many_tiles(dev, oracle, L):
 
 
 @pytest.mark.tuning
-@pytest.mark.parametrize("variant", [150])
+@pytest.mark.parametrize("variant", [150, 303])
 @pytest.mark.parametrize("L", [901, 1024, 2200])
 def test_crc128_long_keys_6bit_tables(dev, oracle, L, variant):
-    """Tuning variant 150: the long-key CRC-32C on r02's 6-bit-slice tables."""
+    """Tuning variants 150 / 303: the long-key CRC-32C on r02's 6-bit-slice tables / on 11-bit slices."""
     rng = np.random.default_rng(L + 5)
     k = rng.integers(0, 256, (20_001, L), dtype=np.uint8)
     with P.tuning(variant):
