@@ -152,8 +152,9 @@ __global__ __launch_bounds__(64) void k_bucket_colscan(u32 *__restrict__ counts,
 // (a load wait also waits for older stores), then adds the sums of the waves
 // before it: one or two memory round trips instead of nchunks / 16.
 constexpr int kCsWaves = 16;
-__device__ __forceinline__ void chunkscan_block(u32 blk, u32 *__restrict__ chunks, u64 nchunks, u32 nranks,
-                                                u64 *__restrict__ totals) {
+// Returns (last wave, r < nranks) rank r's total, else 0.
+__device__ __forceinline__ u64 chunkscan_block(u32 blk, u32 *__restrict__ chunks, u64 nchunks, u32 nranks,
+                                               u64 *__restrict__ totals) {
   __shared__ u32 wsum[kCsWaves][64];
   const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const u32 r = blk * 64 + lane;
@@ -184,12 +185,38 @@ __device__ __forceinline__ void chunkscan_block(u32 blk, u32 *__restrict__ chunk
         run += v[j];
       }
     }
-    if (wave == kCsWaves - 1) totals[r] = run;
+    if (wave == kCsWaves - 1) {
+      totals[r] = run;
+      return run;
+    }
   }
+  return 0;
 }
 __global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan(u32 *__restrict__ chunks, u64 nchunks,
                                                                     u32 nranks, u64 *__restrict__ totals) {
   chunkscan_block(blockIdx.x, chunks, nchunks, nranks, totals);
+}
+// The tile-local two passes' chunk scan: it also turns each block's 64 rank
+// totals into in-block exclusive prefixes inpre[r] and the block's sum
+// bsum[blk] (n < 2^32: u32), so that pass 2 forms the bucket bases itself
+// (k_bucket_tl_pass2: the prefix of bsum + inpre) and no k_bucket_base launch
+// runs between the two.
+__global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan_tl(u32 *__restrict__ chunks, u64 nchunks,
+                                                                       u32 nranks, u64 *__restrict__ totals,
+                                                                       u32 *__restrict__ inpre,
+                                                                       u32 *__restrict__ bsum) {
+  const u32 t = (u32)chunkscan_block(blockIdx.x, chunks, nchunks, nranks, totals);
+  const u32 lane = threadIdx.x & 63, r = blockIdx.x * 64 + lane;
+  if ((threadIdx.x >> 6) == kCsWaves - 1) {
+    u32 x = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(x, o);
+      if (lane >= (u32)o) x += y;
+    }
+    if (r < nranks) inpre[r] = x - t;
+    if (lane == 63) bsum[blockIdx.x] = x;
+  }
 }
 // Two independent chunk scans in one launch (two-pass bucketing: the fine
 // buckets' count-chunk sums and the ranks' count-chunk histograms): blocks
@@ -1124,7 +1151,8 @@ struct TwoPassTL {
   u32 sgmajor;                // segment order: 0 = f-major (all of f, then f + 1), 1 = chunk-range-major
   uint16_t *startsF;          // [ntiles][F] tile-local first row of fine bucket f
   u32 *chunkcnt;              // [nchunks][nranks] rank histogram of chunk g; after the scan its exclusive prefix
-  const u64 *base;            // [nranks] first final slot of bucket r
+  u32 *inpre, *bsum;          // bucket bases = prefix of bsum[r / 64] + inpre[r] (k_bucket_chunkscan_tl)
+  u64 *offsets;               // [nranks + 1] the caller's bucket offsets (pass 2 writes them)
   uint8_t *ikeys;             // [n][L] key rows, each tile sorted by f in place
   uint16_t *ilidx;            // [n] index of the row's key inside its tile
   __device__ __forceinline__ u32 tile_n(u64 t) const {
@@ -1254,6 +1282,16 @@ void k_bucket_tl_pass2(FastMod rk, u32 nranks, TwoPassTL tp, Out out) {
   __shared__ u32 tcount[kTpMaxDigits];
   __shared__ u32 scan_scratch[W];
   __shared__ u32 s_len;
+  __shared__ u32 bpre[kBucketMaxRanks / 64];  // first final slot of each block of 64 ranks
+  static_assert(kBucketMaxRanks / 64 <= kB, "one thread per 64-rank block");
+  {
+    const u32 nblk = (nranks + 63) / 64;
+    const u32 v = threadIdx.x < nblk ? tp.bsum[threadIdx.x] : 0u;
+    const u32 e = block_exclusive_scan<W>(v, scan_scratch);
+    if (threadIdx.x < nblk) bpre[threadIdx.x] = e;
+    if (blockIdx.x == 0 && threadIdx.x == 0) tp.offsets[nranks] = (u64)tp.n;
+    __syncthreads();
+  }
   const RunTab<false> run{runt, tp.C};
   const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u32 q0 = wave * kSub + lane;
@@ -1285,7 +1323,11 @@ void k_bucket_tl_pass2(FastMod rk, u32 nranks, TwoPassTL tp, Out out) {
     }
     if (threadIdx.x < tp.C) {
       const u32 r = threadIdx.x * tp.F + f;
-      if (r < nranks) running[threadIdx.x] = (u32)tp.base[r] + tp.chunkcnt[g0 * nranks + r];
+      if (r < nranks) {
+        const u32 base = bpre[r >> 6] + tp.inpre[r];
+        if (sg == 0) tp.offsets[r] = base;  // (every rank once: its fine bucket's first segment)
+        running[threadIdx.x] = base + tp.chunkcnt[g0 * nranks + r];
+      }
     }
     const u32 before = block_exclusive_scan<W>(mine, scan_scratch);
 #pragma unroll

@@ -205,7 +205,8 @@ static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &ou
 
 // The tile-local two-pass sort (bucket.h k_bucket_tl_*): pass 1 (sorts
 // each tile by f in place, counts ranks per chunk), the rank scan down the
-// chunks, the bucket bases, pass 2 (gathers the f-runs of each segment, sorts
+// chunks (and in-block prefixes of the rank totals), pass 2 (forms the bucket
+// bases and writes bucket_offsets, gathers the f-runs of each segment, sorts
 // by c, stores at the final slots).  Pass 1 in W1 x KPL1 (one tile) @ PER_CU1,
 // pass 2 in W x KPL @ PER_CU.
 template <int L, class Out, int W, int KPL, int PER_CU, int W1, int KPL1, int PER_CU1, int PROBE = 0>
@@ -225,9 +226,8 @@ static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, c
   unsigned g1 = (unsigned)std::min<u64>(tl.nchunks, cus * PER_CU1);
   if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous chunk order (TileOrder)
   f1<<<g1, W1 * 64, b1, st>>>(a.k, a.rk, a.nranks, tl);
-  k_bucket_chunkscan<<<(a.nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(tl.chunkcnt, tl.nchunks, a.nranks, w.totals);
-  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, a.nranks, w.base, bucket_offsets, tl.fbits, nullptr, nullptr,
-                                            nullptr);
+  k_bucket_chunkscan_tl<<<(a.nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(tl.chunkcnt, tl.nchunks, a.nranks,
+                                                                       w.totals, tl.inpre, tl.bsum);
   unsigned g2 = (unsigned)std::min<u64>(tl.nseg, cus * PER_CU);
   if (g2 >= 8) g2 &= ~7u;
   f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tl, out);
@@ -374,7 +374,9 @@ static int bucket_tl(const BucketArgs &a, const BucketWs &w, size_t keysize, con
   tl.sgmajor = hook_tl_sgmajor(false);
   tl.startsF = w.tl_starts;
   tl.chunkcnt = w.tl_chunkcnt;
-  tl.base = w.base;
+  tl.inpre = reinterpret_cast<u32 *>(w.base);  // (nranks x u64 of space, unused here: 2 x nranks u32)
+  tl.bsum = reinterpret_cast<u32 *>(w.base) + a.nranks;
+  tl.offsets = bucket_offsets;
   tl.ikeys = w.tl_keys;
   tl.ilidx = w.tl_lidx;
   return keysize == 8    ? launch_tl_sel<8, Out>(a, tl, out, w, bucket_offsets, st, dev)
