@@ -285,14 +285,13 @@ template <int L, class Out>
 static int launch_tl_sel(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
                          uint64_t *bucket_offsets, hipStream_t st, int dev) {
   if (int rc = hook_tl_shape<L, Out>(a, tl, out, w, bucket_offsets, st, dev); rc != kNoVariant) return rc;
-  if constexpr (L == 32 && !Out::kPair8)
+  // 16-B keys' pass 2 in 8 x 4 @ 2 (8 x 8 spilled 22 VGPRs: arrays -0.5 /
+  // -3.1 % at 4096 / 2048 ranks, records from 4 x 4 @ 4 -4.9 %,
+  // profiles/r06/ab/bucket_16_tl_pass2_shapes.log)
+  if constexpr ((L == 32 && !Out::kPair8) || L == 16)
     return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
   else if constexpr (L == 32)
     return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
-  else if constexpr (L == 16 && Out::kPair8)
-    return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
-  else if constexpr (L == 16)
-    return launch_tl<L, Out, 8, 8, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
   else if constexpr (L == 8 && !Out::kPair8)
     return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
   else

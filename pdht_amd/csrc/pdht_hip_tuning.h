@@ -85,9 +85,12 @@ extern "C" {
  *                     ahead of pass 1, pass 1 writing global fine-bucket runs) instead
  *                     of the tile-local one (r06); 202 and 264-272 imply it
  *            291-293  tile-local two passes: pass 2 in 4x8@4 / 8x4@2; pass 1 in
- *                     16x4@1 (4096-key tiles, 1024 threads) (8/16-B keys)
+ *                     16 waves @ 1 on the product's tiles (1024 threads) (8/16-B keys)
  *            294/295  tile-local pass 1 on 8192-key tiles (16x8@1), pass-2 gathers of
  *                     runs twice as long (8/16-B keys); 295 on the balanced digit split
+ *                304  16-B keys' tile-local pass 2 in r06's first shapes (arrays 8x8@2,
+ *                     records 4x4@4)
+ *                305  32-B records' tile-local pass 2 in 8x4@2
  *                298  timing probe: tile-local pass 2 reading contiguous rows instead of
  *                     gathering its f-runs (wrong outputs; 8/16-B keys)
  *                302  tile-local, 16-B keys: pass 1 in 8x8 (4096-key tiles; spills 23 VGPRs,

@@ -83,29 +83,42 @@ static int hook_two_pass_shape(const BucketArgs &a, const TwoPass &tp, const Out
 }
 
 // Shapes of the tile-local two passes (r06).  291: pass 2 in 4 x 8 @ 4;
-// 292: pass 2 in 8 x 4 @ 2; 293: pass 1 in 16 x 4 (4096-key tiles, 1024
-// threads) @ 1; 294: pass 1 on 8192-key tiles (16 x 8 @ 1; hook_tl_tile_shift),
-// pass-2 runs twice as long; 295: 294 on the balanced digit split.
+// 292: pass 2 in 8 x 4 @ 2; 293: pass 1 in 16 waves (1024 threads) @ 1 on
+// the product's tiles; 294: pass 1 on 8192-key tiles (16 x 8 @ 1;
+// hook_tl_tile_shift), pass-2 runs twice as long; 295: 294 on the balanced
+// digit split.  Pass 1 otherwise as the product's (8 x 8 @ 2 on 4096-key
+// tiles for 8-B keys, 8 x 4 @ 2 on 2048-key tiles for 16-B keys).
 template <int L, class Out>
 static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
                          uint64_t *bucket_offsets, hipStream_t st, int dev) {
   const int v = tuning_variant();
   if constexpr (L <= 16) {
+    constexpr int K1 = L == 8 ? 8 : 4;  // pass-1 keys per lane at the product's tile
     if constexpr (L == 16)
-      if (v == 302) {  // pass 1 in 8 x 8 (4096-key tiles, hook_tl_tile_shift), pass 2 as the product's
+      if (v == 302) {  // pass 1 in 8 x 8 (4096-key tiles, hook_tl_tile_shift), pass 2 as 304
         if constexpr (Out::kPair8)
           return launch_tl<L, Out, 4, 4, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
         else
           return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
       }
+    if constexpr (L == 16)
+      if (v == 304) {  // 16-B keys' pass 2 before r06's last shape change: arrays 8 x 8 @ 2, records 4 x 4 @ 4
+        if constexpr (Out::kPair8)
+          return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+        else
+          return launch_tl<L, Out, 8, 8, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+      }
     if (v == 298)  // timing probe: pass 2 reading contiguous rows (wrong outputs)
-      return launch_tl<L, Out, 8, 8, 2, 8, 8, 2, 1>(a, tl, out, w, bucket_offsets, st, dev);
-    if (v == 291) return launch_tl<L, Out, 4, 8, 4, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
-    if (v == 292) return launch_tl<L, Out, 8, 4, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
-    if (v == 293) return launch_tl<L, Out, 8, 8, 2, 16, 4, 1>(a, tl, out, w, bucket_offsets, st, dev);
+      return launch_tl<L, Out, 8, 8, 2, 8, K1, 2, 1>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 291) return launch_tl<L, Out, 4, 8, 4, 8, K1, 2>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 292) return launch_tl<L, Out, 8, 4, 2, 8, K1, 2>(a, tl, out, w, bucket_offsets, st, dev);
+    if (v == 293) return launch_tl<L, Out, 8, 8, 2, 16, K1 / 2, 1>(a, tl, out, w, bucket_offsets, st, dev);
     if (v == 294 || v == 295 || v == 297)
       return launch_tl<L, Out, 8, 8, 2, 16, 8, 1>(a, tl, out, w, bucket_offsets, st, dev);
   }
+  if constexpr (L == 32 && Out::kPair8)
+    if (v == 305)  // 32-B records' pass 2 in 8 x 4 @ 2 (the arrays' shape)
+      return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
   return kNoVariant;
 }
 
