@@ -1132,8 +1132,9 @@ void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
 //          count-chunk of ct tiles it also keeps the rank histogram (u16
 //          pairs in LDS) -> chunkcnt[g][r]: the counting the old count kernel
 //          did, without a second read of the keys;
-//   scans: chunkcnt down the chunks per rank (k_bucket_chunkscan) + bucket
-//          bases (k_bucket_base);
+//   scan:  chunkcnt down the chunks per rank, and in-block prefixes of the
+//          rank totals (k_bucket_chunkscan_tl); pass 2 forms the bucket
+//          bases from those (no k_bucket_base launch);
 //   pass 2 (k_bucket_tl_pass2): per segment = (f, a range of count-chunks),
 //          GATHER the f-runs of the segment's tiles (each run ~TILE / F
 //          keys, contiguous) through an LDS row map, sort by the coarse
