@@ -1,6 +1,6 @@
-"""The README's round-5 measurement table is recomputable from committed
-profiles: every row equals what tools/hyg_summary.py derives from
-profiles/r05/hyg/<config>/ (the bench line and the rocprofv3 kernel trace of
+"""The README's round-5 and round-6 measurement tables are recomputable from
+committed profiles: every row equals what tools/hyg_summary.py derives from
+profiles/r0N/hyg/<config>/ (the bench line and the rocprofv3 kernel trace of
 the same run).  CPU only."""
 import json
 import os
@@ -10,12 +10,14 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HYG = os.path.join(ROOT, "profiles", "r05", "hyg")
+# README section title -> (profiles directory, rows at least)
+TABLES = {"## Round 6: every line": ("r06", 13), "## Round 5": ("r05", 11)}
 
 
-def readme_rows():
+def readme_rows(title):
     text = open(os.path.join(ROOT, "README.md")).read()
-    sec = text[text.index("## Round 5"):]
+    sec = text[text.index(title):]
+    sec = sec[:sec.find("\n## ", 1)] if "\n## " in sec[1:] else sec
     rows = {}
     for ln in sec.splitlines():
         if not ln.startswith("| "):
@@ -27,13 +29,17 @@ def readme_rows():
     return rows
 
 
-@pytest.mark.skipif(not os.path.isdir(HYG), reason="no r05 profiles")
-def test_readme_r05_table_matches_profiles():
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "hyg_summary.py"), HYG],
+@pytest.mark.parametrize("title", sorted(TABLES))
+def test_readme_table_matches_profiles(title):
+    rnd, least = TABLES[title]
+    hyg = os.path.join(ROOT, "profiles", rnd, "hyg")
+    if not os.path.isdir(hyg):
+        pytest.skip(f"no {rnd} profiles")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "hyg_summary.py"), hyg],
                          capture_output=True, text=True, check=True).stdout
     got = {r["cfg"]: r for r in map(json.loads, out.splitlines())}
-    rows = readme_rows()
-    assert len(rows) >= 11, sorted(rows)
+    rows = readme_rows(title)
+    assert len(rows) >= least, sorted(rows)
     for cfg, c in rows.items():
         r = got[cfg]
         assert c[1] == f"`{r['kernel']}`", cfg

@@ -14,7 +14,7 @@ tools/gpu_session.sh hyg_<cfg>).  For each config it prints
   * their ratio, so a reader can check that the event timing and the kernel
     durations agree.
 
-  python tools/hyg_summary.py profiles/r05/hyg [--md]
+  python tools/hyg_summary.py profiles/r06/hyg [--md]
 """
 import csv
 import json
@@ -34,6 +34,8 @@ STEP_KERNELS = {
     # (late r05: the two-pass count kernel scans its fine counts itself, no colscan launch)
     "bucket8k": ["k_bucket_count_tp", "k_bucket_chunkscan2", "k_bucket_base", "k_bucket_pass1",
                  "k_bucket_pass2"],
+    # r06: the tile-local two passes (pass 2 forms the bucket bases: no k_bucket_base)
+    "bucket8k_tl": ["k_bucket_tl_pass1", "k_bucket_chunkscan_tl", "k_bucket_tl_pass2"],
 }
 
 
@@ -78,7 +80,7 @@ def step_kernel_us(cfg, trace, line):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     steps = line["steps"]
     if cfg in STEP_KERNELS:
-        pats = STEP_KERNELS[cfg]
+        pats = STEP_KERNELS[cfg + "_tl" if line["config"]["kernel"].startswith("k_bucket_tl") else cfg]
         is_step = lambda nm: any(p in nm for p in pats)  # noqa: E731
         per = len(pats)
     else:
