@@ -124,7 +124,7 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * (device) must hold pdht_bucket_workspace_bytes(n, keysize, nranks): the
  * per-tile counts and, for 8/16/32-B keys at the rank counts that take the
  * two-pass sort (from 1536 / 1025 / 2049 ranks for 8 / 16 / 32-B keys), its
- * intermediate (about n x (keysize + 4) bytes). */
+ * intermediate (about n x (keysize + 2) bytes). */
 size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
                           uint32_t nptes, uint32_t nranks, void *workspace,

@@ -16,16 +16,15 @@
 //                      slots in index order (stable).
 //
 // Scatter kernels:
-//   _staged  (8/16/32-B keys, nranks <= 2048; default) sorts the tile by bucket
-//            in LDS first and then writes each bucket's run of the tile with
-//            consecutive lanes, so stores are coalesced runs, not 64 scattered
-//            8-byte pieces per instruction; tiles are dealt to XCDs in
-//            contiguous ranges so that the runs of neighbouring tiles meet in
-//            the same L2 and leave it as whole lines.
-//   _reg     (8/16/32-B keys, larger nranks) scatters straight from VGPRs.
-//   _wg      (any key length) re-reads keys from L2 in the scatter pass.
-// Lanes holding the same bucket find each other with ceil(log2 nranks)
-// ballots; the group leader advances the bucket's slot in LDS.
+//   _staged  (8/16/32-B keys below the two-pass threshold) sorts the tile by
+//            bucket in LDS first and then writes each bucket's run of the
+//            tile with consecutive lanes, so stores are coalesced runs, not 64
+//            scattered 8-byte pieces per instruction; tiles are dealt to XCDs
+//            in contiguous ranges so that the runs of neighbouring tiles meet
+//            in the same L2 and leave it as whole lines.
+//   _wg      (any other key length) re-reads keys from L2 in the scatter pass.
+// From the two-pass threshold up, 8/16/32-B keys take the tile-local two
+// passes (k_bucket_tl_*, below) instead of the count + scatter chain.
 #pragma once
 
 #include "kernels.h"
@@ -218,18 +217,6 @@ __global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan_tl(u32 *__re
     if (lane == 63) bsum[blockIdx.x] = x;
   }
 }
-// Two independent chunk scans in one launch (two-pass bucketing: the fine
-// buckets' count-chunk sums and the ranks' count-chunk histograms): blocks
-// [0, nb1) scan the first, the rest the second.
-__global__ __launch_bounds__(64 * kCsWaves) void k_bucket_chunkscan2(u32 *__restrict__ c1, u64 n1, u32 w1,
-                                                                     u64 *__restrict__ t1, u32 nb1,
-                                                                     u32 *__restrict__ c2, u64 n2, u32 w2,
-                                                                     u64 *__restrict__ t2) {
-  if (blockIdx.x < nb1)
-    chunkscan_block(blockIdx.x, c1, n1, w1, t1);
-  else
-    chunkscan_block(blockIdx.x - nb1, c2, n2, w2, t2);
-}
 
 // ------------------------------------------------------------- helpers ---
 // Lanes whose r equals mine (AND of per-bit ballots; invalid lanes excluded).
@@ -270,15 +257,12 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T *scratch /* NW words */
 // start at w * stride (stride = nranks, rounded up to even when packed so a
 // word never straddles two waves).
 // Exclusive scan of the per-rank totals (one workgroup of kBaseThreads, each
-// thread a run of consecutive ranks) -> bucket offsets; with fbase (two-pass
-// bucketing), also the first intermediate row of every fine bucket f = r mod
-// F: the exclusive scan of the fine-bucket totals ftot.
+// thread a run of consecutive ranks) -> bucket offsets; zeroes the scatter's
+// per-XCD tile tickets.
 constexpr u32 kBaseThreads = 1024;
 __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restrict__ totals, u32 nranks,
                                                               u64 *__restrict__ base,
-                                                              u64 *__restrict__ offsets_out, u32 fbits,
-                                                              const u64 *__restrict__ ftot,
-                                                              u64 *__restrict__ fbase,
+                                                              u64 *__restrict__ offsets_out,
                                                               u32 *__restrict__ tickets) {
   // the totals pass through LDS so that global loads and stores are
   // lane-contiguous (a thread's run of consecutive ranks would make every
@@ -314,12 +298,6 @@ __global__ __launch_bounds__(kBaseThreads) void k_bucket_base(const u64 *__restr
   for (u32 r = threadIdx.x; r < nranks; r += kBaseThreads) {
     base[r] = tot[r];
     offsets_out[r] = tot[r];
-  }
-  if (fbase) {
-    const u32 F = 1u << fbits;  // <= kTpMaxDigits
-    const u64 fs = threadIdx.x < F ? ftot[threadIdx.x] : 0;
-    const u64 fb = block_exclusive_scan<kBaseThreads / 64, u64>(fs, scratch);
-    if (threadIdx.x < F) fbase[threadIdx.x] = fb;
   }
 }
 
@@ -776,35 +754,13 @@ void k_bucket_scatter_staged(
   }
 }
 
-// ----------------------------------------------------- two-pass bucketing ---
-// One pass writes, per 4096-key tile, one run per bucket into every output
-// array: at 1024 ranks runs of 4 keys (32 B of an 8-B array, 16 B of a 4-B
-// one), and the write path runs at ~1.3-3 TB/s on such runs against ~4.5 on
-// >= 128-B runs (tools/scatter_probe.hip).  Two stable passes over the two
-// digits of rank = c * F + f (F = 2^fbits fine buckets, C = ceil(nranks / F)
-// coarse ones, F, C ~ sqrt(nranks)) write runs of ~4096 / F and ~4096 / C
-// keys, at the price of an intermediate array (key row + original index):
-//   pass 1 (k_bucket_pass1): per counting tile, the tile's keys in fine-bucket
-//          order into the intermediate at fbase[f] + (fine-f keys of earlier
-//          tiles), stable: the intermediate is ordered by (f, original index);
-//   pass 2 (k_bucket_pass2): per segment = (f, SG consecutive count-chunks
-//          of kTpChunkTiles tiles), a contiguous stretch of the intermediate that
-//          holds, in original order, the fine-f keys of those tiles.  Sorted
-//          by c in sub-tiles of 4096 keys, each key goes to its final slot:
-//          bucket r = c * F + f receives the segment's keys at base[r] +
-//          chunkcnt[g0][r] onwards, in order.
-// Both passes take their positions from the single pass's per-tile counts
-// (count kernel + scans): no extra counting and no inter-workgroup waits.
-#ifndef PDHT_TP_TILE  // compile-time experiments only (make exp EXP=-DPDHT_TP_TILE=...)
-#define PDHT_TP_TILE 4096
-#endif
-#ifndef PDHT_TP_CHUNK_TILES
-#define PDHT_TP_CHUNK_TILES 8
-#endif
+// ------------------------------------------------------------ two passes ---
+// Sizes shared by the two-pass sort below (k_bucket_tl_*).  The r02-r05 form
+// (a counting kernel ahead of pass 1, pass 1 writing global fine-bucket runs)
+// lives in tuning/bucket_two_pass_r05.h, compiled into the A/B library only.
 #ifndef PDHT_TP_SEG_KEYS
 #define PDHT_TP_SEG_KEYS 3840
 #endif
-constexpr u32 kTpCountTile = PDHT_TP_TILE;  // counting tile = pass-1 unit
 // Pass-2 segment: ~this many keys of one fine bucket.  A segment's length
 // is a sum of per-chunk counts (binomial): at a mean of 4096 keys (r02-r05)
 // half the segments held a few dozen keys more than one 4096-key sub-tile
@@ -812,86 +768,13 @@ constexpr u32 kTpCountTile = PDHT_TP_TILE;  // counting tile = pass-1 unit
 // 4096 - 4 sigma = 3840 keeps them in one (and in whole 2048 / 1024-key
 // sub-tiles): 8-B keys at 8192 / 2048 ranks -10.6 / -6.7 %, 16-B keys at
 // 4096 -4.5 %, 8-B records -1.6 %, 32-B keys within +-1.2 %
-// (profiles/r05/ab/bucket_pass2_segment_keys.log).
+// (r05 form, profiles/r05/ab/bucket_pass2_segment_keys.log).
 constexpr u32 kTpSegKeys = PDHT_TP_SEG_KEYS;
 // F, C <= 256.  nranks <= 8192 = 2^13: the balanced split gives F = 2^7,
 // C = 2^6; the fine-plus split of 8/16-B array outputs (late r03,
 // pdht_bucket.hip) F = 2^8 -- at this bound -- and C = 2^5.  The launcher
 // checks both before any two-pass launch.
 constexpr u32 kTpMaxDigits = 256;
-constexpr u32 kTpChunkTiles = PDHT_TP_CHUNK_TILES;  // counting tiles per count-chunk (one count workgroup)
-struct TwoPass {
-  u32 fbits, F, C, cbits;
-  const u32 *countsF;   // [ntiles][F] fine-bucket keys of tile t before it in its fchunk-tile chunk
-  const u32 *chunksF;   // [ntiles/fchunk][F] ... of the chunks before it
-  u32 fchunk;           // tiles per fine-count chunk
-  const u64 *totalsF;   // [F] keys per fine bucket
-  const u32 *chunkcnt;  // [nchunks][nranks] keys of rank r in the count-chunks before chunk g
-  const u64 *base;      // [nranks] first final slot of bucket r
-  const u64 *fbase;     // [F] first intermediate row of fine bucket f
-  uint8_t *ikeys;       // [n][L] intermediate key rows
-  u32 *iidx;            // [n] intermediate original indices
-  u64 ntiles, nchunks;  // counting tiles; count-chunks of kTpChunkTiles tiles
-  u64 SG, nsegf, nseg;  // count-chunks per segment (about); segments per f; segments
-  // keys of fine bucket f in the tiles before tile t (t <= ntiles)
-  __device__ __forceinline__ u32 fine_before(u64 t, u32 f) const {
-    return t < ntiles ? countsF[t * F + f] + chunksF[(t / fchunk) * F + f] : (u32)totalsF[f];
-  }
-};
-
-// Two-pass counting.  One workgroup per count-chunk of kTpChunkTiles
-// counting tiles: the fine-bucket histogram of every tile -> countsF[t][f],
-// and the rank histogram of the whole chunk -> chunkcnt[g][r].  The single
-// pass's per-tile rank rows are as large as the keys at high rank counts
-// (4096 tiles x 8192 ranks x 4 B = 128 MB for 16M keys, written, scanned and
-// read again); these are nranks/F and kTpChunkTiles times smaller.
-// With chunksF (fchunk = kTpChunkTiles), countsF[t][f] is already the
-// exclusive scan down the chunk and chunksF[g][f] the chunk's sum, so no
-// column scan of countsF follows.
-template <int L>
-__global__ __launch_bounds__(kBlock) void k_bucket_count_tp(const uint8_t *__restrict__ keys, u64 n, FastMod rk,
-                                                            u32 nranks, u32 F, u32 *__restrict__ countsF,
-                                                            u32 *__restrict__ chunkcnt, u64 ntiles,
-                                                            u32 *__restrict__ chunksF) {
-  constexpr int U = 128 / L;
-  extern __shared__ u32 hist[];  // [nranks]
-  __shared__ u32 fh[kTpMaxDigits];
-  const u32 fmask = F - 1;
-  const u64 nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
-  for (u64 g = blockIdx.x; g < nchunks; g += gridDim.x) {
-    for (u32 r = threadIdx.x; r < nranks; r += kBlock) hist[r] = 0;
-    u32 facc = 0;  // thread f < F: fine-f keys of the chunk's tiles so far
-    const u64 t1 = min((g + 1) * kTpChunkTiles, ntiles);
-    for (u64 t = g * kTpChunkTiles; t < t1; ++t) {
-      if (threadIdx.x < F) fh[threadIdx.x] = 0;
-      __syncthreads();
-      const u64 k0 = t * kTpCountTile;
-      const u64 kend = min(k0 + kTpCountTile, n);
-      for (u64 i = k0 + threadIdx.x; i < kend; i += (u64)kBlock * U) {
-        RegReader<L / 4> kr[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) load_key_regs<L, true>(keys, min(i + u * kBlock, n - 1), kr[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (i + u * kBlock < kend) {
-            const u32 r = (u32)rk.mod(city64(kr[u], (u64)L));
-            atomicAdd(&hist[r], 1u);
-            atomicAdd(&fh[r & fmask], 1u);
-          }
-      }
-      __syncthreads();
-      if (threadIdx.x < F) {
-        const u32 c = fh[threadIdx.x];
-        countsF[t * F + threadIdx.x] = chunksF ? facc : c;
-        facc += c;
-      }
-    }
-    if (chunksF && threadIdx.x < F) chunksF[g * F + threadIdx.x] = facc;
-    __syncthreads();
-    for (u32 r = threadIdx.x; r < nranks; r += kBlock) chunkcnt[g * nranks + r] = hist[r];
-    __syncthreads();
-  }
-}
 
 // Digit-run tables and scan of a tile sorted by a digit < ND <= kB (one thread
 // per digit): on return run[w][d] = tile-local start of wave w's keys of
@@ -918,230 +801,35 @@ __device__ __forceinline__ void digit_starts(const RunTab<false> &run, u32 ND, u
   }
 }
 
-// Pass-1 units are the counting tiles (kTpCountTile keys); both passes work
-// through their units in sub-tiles of W x KPL x 64 keys, carrying each
-// digit's next slot across sub-tiles.  Runs stay long with small sub-tiles
-// (1024 keys over 32 digits: 32-key runs), and small sub-tiles keep LDS and
-// VGPRs per workgroup low, so that several workgroups per CU overlap one
-// another's load / rank / store phases.
-// r02-r03 shape of both passes (4 waves x 8 keys per lane, 4 WG/CU); since r04
-// pass 1 runs 8 x 8 @ 2 and 16-B keys' pass 2 too (launch_two_pass_sel).
-constexpr int kTpW = 4, kTpKPL = 8, kTpPerCu = 4;
-template <int W, int KPL>
-constexpr size_t pass1_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 2 + 1); }
-template <int W, int KPL>
-constexpr size_t pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
-
-template <int L, int W = kTpW, int KPL = kTpKPL, int WPE = 8>
-__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass1(const uint8_t *__restrict__ keys, u64 n, FastMod rk, TwoPass tp) {
-  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
-  static_assert(kTpCountTile % kTile == 0, "sub-tiles of a counting tile");
-  extern __shared__ u64 lds64[];
-  u64 *stage = lds64;                                            // [kTile] key pieces
-  uint16_t *sidx = reinterpret_cast<uint16_t *>(stage + kTile);  // [kTile] sub-tile-local index
-  uint8_t *sdig = reinterpret_cast<uint8_t *>(sidx + kTile);     // [kTile] fine digit
-  __shared__ u32 runt[W * kTpMaxDigits];
-  __shared__ u32 running[kTpMaxDigits];  // next intermediate row of fine bucket f
-  __shared__ u32 delta[kTpMaxDigits];
-  __shared__ u32 tcount[kTpMaxDigits];
-  __shared__ u32 scan_scratch[W];
-  const RunTab<false> run{runt, tp.F};
-  const u32 fmask = tp.F - 1;
-  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const u32 q0 = wave * kSub + lane;
-  for (TileOrder o(tp.ntiles); o.t < o.end; o.t += o.step) {
-    const u64 t = o.t;
-    const u64 tbase = t * kTpCountTile;
-    const u32 ttn = (u32)min((u64)kTpCountTile, n - tbase);
-    // the tile's rows in fine bucket f follow those of the earlier tiles
-    if (threadIdx.x < tp.F) running[threadIdx.x] = (u32)tp.fbase[threadIdx.x] + tp.fine_before(t, threadIdx.x);
-    for (u32 s0 = 0; s0 < ttn; s0 += kTile) {
-      const u32 tn = min(kTile, ttn - s0);
-      const u64 sbase = tbase + s0;
-      for (u32 j = threadIdx.x; j < W * tp.F; j += kB) runt[j] = 0;
-      RegReader<L / 4> kr[KPL];
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(sbase + q0 + g * 64, n - 1), kr[g]);
-      u32 ff[KPL];
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) ff[g] = (u32)rk.mod(city64(kr[g], (u64)L)) & fmask;
-      __syncthreads();
-#pragma unroll
-      for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < tn) run.add(wave, ff[g], 1u);
-      __syncthreads();
-      digit_starts<W>(run, tp.F, delta, tcount, scan_scratch, [&](u32 f) { return running[f]; });
-      __syncthreads();
-      u32 lp[KPL];
-      rank_groups<KPL>(run, wave, ff, q0, tn, tp.fbits, lp);
-#pragma unroll
-      for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < tn) {
-          stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
-          sidx[lp[g]] = (uint16_t)(q0 + g * 64);
-          sdig[lp[g]] = (uint8_t)ff[g];
-        }
-      __syncthreads();
-      u32 gp[KPL];
-#pragma unroll
-      for (int jj = 0; jj < KPL; ++jj) {
-        const u32 j = jj * kB + threadIdx.x;
-        if (j < tn) {
-          gp[jj] = delta[sdig[j]] + j;
-          tp.iidx[gp[jj]] = (u32)(sbase + sidx[j]);
-          *reinterpret_cast<u64 *>(tp.ikeys + (u64)gp[jj] * L) = stage[j];
-        }
-      }
-#pragma unroll
-      for (int c = 1; c < L / 8; ++c) {
-        __syncthreads();
-#pragma unroll
-        for (int g = 0; g < KPL; ++g)
-          if (q0 + g * 64 < tn) stage[lp[g]] = (u64)kr[g].d[2 * c] | ((u64)kr[g].d[2 * c + 1] << 32);
-        __syncthreads();
-#pragma unroll
-        for (int jj = 0; jj < KPL; ++jj) {
-          const u32 j = jj * kB + threadIdx.x;
-          if (j < tn) *reinterpret_cast<u64 *>(tp.ikeys + (u64)gp[jj] * L + 8 * c) = stage[j];
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x < tp.F) running[threadIdx.x] += tcount[threadIdx.x];
-    }
-    __syncthreads();
-  }
-}
-
-// ONE (8-B keys into arrays, the default there since late r05): the sub-tile
-// stages {key, index} instead of {digest, index} and hashes each key a
-// second time in the store phase, so all four outputs of a key leave in one
-// phase -- two barriers and one LDS round per sub-tile fewer than staging the
-// digest first and the key bytes after it (staged_store).  Interleaved, 16M
-// keys at 8192 ranks: -1.0 to -1.3 % (profiles/r05/ab/bucket8k_pass2_one_store_phase.log).
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int WPE = 8, bool ONE = (L == 8 && !Out::kPair8)>
-__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_bucket_pass2(FastMod rk, u32 nranks, TwoPass tp, Out out) {
-  static_assert(!ONE || (L == 8 && !Out::kPair8), "one store phase: 8-B keys into arrays");
-  constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
-  extern __shared__ u64 lds64[];
-  u64 *stage = lds64;                                    // [kTile] digests, then key pieces (ONE: keys)
-  u32 *sidx = reinterpret_cast<u32 *>(stage + kTile);  // [kTile] original index
-  __shared__ u32 runt[W * kTpMaxDigits];
-  __shared__ u32 running[kTpMaxDigits];  // next final slot of bucket c*F + f
-  __shared__ u32 delta[kTpMaxDigits];
-  __shared__ u32 tcount[kTpMaxDigits];
-  __shared__ u32 seg[2];  // rows of the segment before it in fine bucket f; its length
-  __shared__ u32 scan_scratch[W];
-  const RunTab<false> run{runt, tp.C};
-  const u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const u32 q0 = wave * kSub + lane;
-  const u32 fbits = tp.fbits;
-  auto coarse = [&](u64 h, u32) { return (u32)rk.mod(h) >> fbits; };
-  for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
-    const u32 f = (u32)(o.t / tp.nsegf);
-    const u64 sg = o.t % tp.nsegf;  // the f-bucket's count-chunks split evenly over nsegf segments
-    const u64 g0 = sg * tp.nchunks / tp.nsegf, g1 = (sg + 1) * tp.nchunks / tp.nsegf;
-    if (threadIdx.x == 0) {
-      const u32 lo = tp.fine_before(g0 * kTpChunkTiles, f);
-      seg[0] = lo;
-      seg[1] = tp.fine_before(min(g1 * kTpChunkTiles, tp.ntiles), f) - lo;
-    }
-    if (threadIdx.x < tp.C) {
-      const u32 r = threadIdx.x * tp.F + f;
-      if (r < nranks) running[threadIdx.x] = (u32)tp.base[r] + tp.chunkcnt[g0 * nranks + r];
-    }
-    __syncthreads();
-    const u32 sstart = (u32)tp.fbase[f] + seg[0], slen = seg[1];
-    for (u32 k0 = 0; k0 < slen; k0 += kTile) {
-      const u32 tn = min(kTile, slen - k0);
-      const u64 p0 = (u64)sstart + k0;
-      for (u32 j = threadIdx.x; j < W * tp.C; j += kB) runt[j] = 0;
-      RegReader<L / 4> kr[KPL];
-      u32 ix[KPL];
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) {
-        const u64 p = p0 + min(q0 + g * 64, tn - 1);
-        load_key_regs<L, true>(tp.ikeys, p, kr[g]);
-        ix[g] = __builtin_nontemporal_load(tp.iidx + p);
-      }
-      u64 h[ONE ? 1 : KPL];
-      u32 cc[KPL];
-#pragma unroll
-      for (int g = 0; g < KPL; ++g) {
-        const u64 hh = city64(kr[g], (u64)L);
-        if constexpr (!ONE) h[g] = hh;
-        cc[g] = coarse(hh, 0u);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < tn) run.add(wave, cc[g], 1u);
-      __syncthreads();
-      digit_starts<W>(run, tp.C, delta, tcount, scan_scratch, [&](u32 c) { return running[c]; });
-      __syncthreads();
-      u32 lp[KPL];
-      rank_groups<KPL>(run, wave, cc, q0, tn, tp.cbits, lp);
-#pragma unroll
-      for (int g = 0; g < KPL; ++g)
-        if (q0 + g * 64 < tn) {
-          if constexpr (ONE)
-            stage[lp[g]] = (u64)kr[g].d[0] | ((u64)kr[g].d[1] << 32);
-          else
-            stage[lp[g]] = h[g];
-          sidx[lp[g]] = ix[g];
-        }
-      __syncthreads();
-      if constexpr (ONE) {
-        // thread j: staged key j -> hash again -> its slot; every output at once
-#pragma unroll
-        for (int jj = 0; jj < KPL; ++jj) {
-          const u32 j = jj * kB + threadIdx.x;
-          if (j < tn) {
-            RegReader<2> r;
-            const u64 key = stage[j];
-            r.d[0] = (u32)key;
-            r.d[1] = (u32)(key >> 32);
-            const u64 hv = city64(r, (u64)L);
-            const u32 slot = delta[coarse(hv, 0u)] + j;
-            out.meta(slot, hv, sidx[j]);
-            if (out.has_keys()) out.key8(slot, 0, key);
-          }
-        }
-      } else {
-        staged_store<L, KPL, kB>(stage, delta, tn, kr, lp, q0, coarse, [&](u32 j) { return (u64)sidx[j]; }, out);
-      }
-      __syncthreads();
-      if (threadIdx.x < tp.C) running[threadIdx.x] += tcount[threadIdx.x];
-    }
-    __syncthreads();
-  }
-}
-
-// -------------------------------------- two-pass bucketing, tile-local runs ---
-// r06 restructure of the two passes.  Above, pass 1
-// writes each tile's fine-bucket runs to GLOBAL fine-bucket positions, so it
-// needs every tile's fine counts scanned first: a counting kernel reads and
-// hashes the whole batch once more ahead of it (count + scans: ~57 of 336 us
-// at 8192 ranks).  Here pass 1 needs nothing ahead of it:
+// ------------------------------------------ two-pass bucketing, tile-local ---
+// One pass writes, per tile, one run per bucket into every output array: at
+// 8192 ranks an 8192-key tile has runs of about one key, and the write path
+// runs at ~1.3-3 TB/s on runs under 64 B against ~4.5 on >= 128-B runs
+// (tools/scatter_probe.hip).  From two_pass_min_ranks() up (pdht_bucket.hip)
+// the batch is sorted stably by the two digits of rank = c * F + f (F = 2^fbits
+// fine buckets, C = ceil(nranks / F) coarse ones, both ~sqrt(nranks)), in
+// passes that write runs of ~TILE / F and ~segment / C keys, at the price of an
+// intermediate (key row + u16 index inside its tile):
 //   pass 1 (k_bucket_tl_pass1): per tile of TILE keys (one sub-tile), sort by
 //          the fine digit f in LDS and write the tile back IN PLACE -- rows
 //          [t*TILE, (t+1)*TILE) of the intermediate, one contiguous store run
 //          per wave instruction -- as key rows + the u16 index inside the
 //          tile, plus the tile's F run starts (u16) startsF[t][f].  Per
 //          count-chunk of ct tiles it also keeps the rank histogram (u16
-//          pairs in LDS) -> chunkcnt[g][r]: the counting the old count kernel
-//          did, without a second read of the keys;
+//          pairs in LDS) -> chunkcnt[g][r], so nothing counts ahead of it;
 //   scan:  chunkcnt down the chunks per rank, and in-block prefixes of the
 //          rank totals (k_bucket_chunkscan_tl); pass 2 forms the bucket
 //          bases from those (no k_bucket_base launch);
 //   pass 2 (k_bucket_tl_pass2): per segment = (f, a range of count-chunks),
 //          GATHER the f-runs of the segment's tiles (each run ~TILE / F
 //          keys, contiguous) through an LDS row map, sort by the coarse
-//          digit c and store every output at its final slot (as
-//          k_bucket_pass2 does).  Original index = tile row base | u16.
-// One launch fewer, no second hash of the batch, pass-1 stores whole lines;
-// the intermediate shrinks from L + 4 to L + 2 bytes per key.
+//          digit c and store every output at its final slot.  Original
+//          index = tile row base | u16.
+// Against the r02-r05 form (tuning/bucket_two_pass_r05.h: a counting kernel
+// reads and hashes the batch ahead of a pass 1 that writes each tile's
+// fine-bucket runs to global positions), one launch and one read of the keys
+// fewer, pass-1 stores are whole lines, and the intermediate shrinks from
+// L + 4 to L + 2 bytes per key.
 constexpr u32 kTlMaxRuns = 512;  // tiles (= f-runs) per pass-2 segment
 struct TwoPassTL {
   u32 fbits, F, C, cbits;

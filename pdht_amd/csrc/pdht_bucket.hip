@@ -10,19 +10,12 @@
 namespace pdht {
 struct BucketWs {
   u32 *counts, *chunks;
-  u64 *totals, *base, *fbase;
+  u64 *totals, *base;
   u32 *tickets;  // [8] per-XCD tile tickets of the dynamic scatter
-  // two-pass sort (8/16/32-B keys): fine-bucket counts per tile (scanned
-  // down each count-chunk) and per count-chunk, fine totals, rank counts per
-  // count-chunk, and the
-  // intermediate ([n][keysize] key rows + [n] original indices)
-  u32 *countsF, *chunksF, *chunkcnt;
-  u64 *totalsF;
-  uint8_t *ikeys;
-  u32 *iidx;
-  // the tile-local two-pass sort (r06, bucket.h k_bucket_tl_*) in the same
-  // region: per-tile f-run starts, per-chunk rank histograms, key rows and
-  // their u16 indices inside the tile
+  // the two-pass region (8/16/32-B keys from two_pass_min_ranks()): the
+  // tile-local sort's per-tile f-run starts, per-chunk rank histograms, key
+  // rows and their u16 indices inside the tile
+  uint8_t *region;
   uint16_t *tl_starts, *tl_lidx;
   u32 *tl_chunkcnt;
   uint8_t *tl_keys;
@@ -55,70 +48,6 @@ static u32 tl_chunk_tiles(u64 ntiles, u32 tshift) {
   while (ct > 1 && ntiles / ct < 512) ct >>= 1;
   return ct;
 }
-// Sized for the smallest tile any scatter kernel uses, plus the two-pass
-// region when the batch can take that path: 8/16/32-B keys from
-// two_pass_min_ranks() up for the output kind (records: `records`; the tuning
-// build forces two passes at any nranks and always reserves it).  The region
-// holds either two-pass form (the r02-r05 one for the A/B build).  16M x 8-B
-// keys at 1024 ranks: 17 MB; from 1536 ranks + 160 MB.
-static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks, bool records) {
-  const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
-  const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
-  BucketWs w{};
-  uint8_t *p = static_cast<uint8_t *>(ws);
-  size_t off = 0;
-  w.counts = reinterpret_cast<u32 *>(p + off);
-  off += round256((size_t)nranks * ntiles * 4);
-  w.chunks = reinterpret_cast<u32 *>(p + off);
-  off += round256((size_t)nranks * nchunks * 4);
-  w.totals = reinterpret_cast<u64 *>(p + off);
-  off += round256((size_t)nranks * 8);
-  w.base = reinterpret_cast<u64 *>(p + off);
-  off += round256((size_t)nranks * 8);
-  w.fbase = reinterpret_cast<u64 *>(p + off);
-  off += round256((size_t)kTpMaxDigits * 8);
-  w.tickets = reinterpret_cast<u32 *>(p + off);
-  off += 256;
-  const bool two_pass = hook_bucket_reserve(
-      two_pass_keysize(keysize) && nranks >= two_pass_min_ranks(keysize, records), keysize);
-  if (two_pass) {
-    // the r02-r05 form: fine counts per tile and chunk, fine totals, rank
-    // counts per chunk, key rows + u32 original indices
-    size_t o = off;
-    const u64 tp_tiles = (n + kTpCountTile - 1) / kTpCountTile;
-    const u64 tp_chunks = (tp_tiles + kTpChunkTiles - 1) / kTpChunkTiles;
-    w.countsF = reinterpret_cast<u32 *>(p + o);
-    o += round256((size_t)tp_tiles * kTpMaxDigits * 4);
-    w.chunksF = reinterpret_cast<u32 *>(p + o);  // rows of kTpChunkTiles (or kBucketChunk) tiles
-    o += round256((size_t)tp_chunks * kTpMaxDigits * 4);
-    w.totalsF = reinterpret_cast<u64 *>(p + o);
-    o += round256((size_t)kTpMaxDigits * 8);
-    w.chunkcnt = reinterpret_cast<u32 *>(p + o);
-    o += round256((size_t)tp_chunks * nranks * 4);
-    w.ikeys = p + o;
-    o += round256(n * keysize);
-    w.iidx = reinterpret_cast<u32 *>(p + o);
-    o += round256(n * 4);
-    // the tile-local form over the same bytes: f-run starts per tile, rank
-    // counts per chunk, key rows + u16 indices inside the tile
-    size_t q = off;
-    const u32 sh = tl_tile_shift(keysize);
-    const u64 tl_tiles = (n + (1ull << sh) - 1) >> sh;
-    const u64 tl_chunks = (tl_tiles + tl_chunk_tiles(tl_tiles, sh) - 1) / tl_chunk_tiles(tl_tiles, sh);
-    w.tl_starts = reinterpret_cast<uint16_t *>(p + q);
-    q += round256((size_t)tl_tiles * kTpMaxDigits * 2);
-    w.tl_chunkcnt = reinterpret_cast<u32 *>(p + q);
-    q += round256((size_t)tl_chunks * nranks * 4);
-    w.tl_keys = p + q;
-    q += round256(n * keysize);
-    w.tl_lidx = reinterpret_cast<uint16_t *>(p + q);
-    q += round256(n * 2);
-    off = std::max(o, q);
-  }
-  w.bytes = off;
-  return w;
-}
-
 static int set_lds(const void *fn, size_t bytes) {
   if (bytes > 65536)
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
@@ -177,32 +106,6 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
 
 
 
-// Pass 1 and pass 2 each take a shape: W waves x KPL keys per lane per
-// sub-tile, PER_CU workgroups per CU (pass 1: W1, KPL1, PER_CU1).  Both run
-// their units in the static XCD-contiguous order (TileOrder; per-XCD tickets
-// gained nothing here, r02 tuning variant 86).
-template <int L, class Out, int W = kTpW, int KPL = kTpKPL, int PER_CU = kTpPerCu, int W1 = W, int KPL1 = KPL,
-          int PER_CU1 = PER_CU, bool ONE = (L == 8 && !Out::kPair8)>
-static int launch_two_pass(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
-  static const char *const names[3] = {"k_bucket_pass2<8B>", "k_bucket_pass2<16B>", "k_bucket_pass2<32B>"};
-  constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;      // waves per SIMD, pass 2
-  constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;  // pass 1
-  const size_t b1 = pass1_lds_bytes<W1, KPL1>(), b2 = pass2_lds_bytes<W, KPL>();
-  auto f1 = &k_bucket_pass1<L, W1, KPL1, WPE1>;
-  auto f2 = &k_bucket_pass2<L, Out, W, KPL, WPE, ONE>;
-  if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
-  if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
-  const u64 cus = (u64)std::max(1, g_dev[dev].cus);
-  unsigned g1 = (unsigned)std::min<u64>(a.ntiles, cus * PER_CU1);
-  if (g1 >= 8) g1 &= ~7u;  // XCD-contiguous tile order (TileOrder)
-  f1<<<g1, W1 * 64, b1, st>>>(a.k, a.n, a.rk, tp);
-  unsigned g2 = (unsigned)std::min<u64>(tp.nseg, cus * PER_CU);
-  if (g2 >= 8) g2 &= ~7u;
-  f2<<<g2, W * 64, b2, st>>>(a.rk, a.nranks, tp, out);
-  g_kernel = names[L == 8 ? 0 : L == 16 ? 1 : 2];
-  return 0;
-}
-
 // The tile-local two-pass sort (bucket.h k_bucket_tl_*): pass 1 (sorts
 // each tile by f in place, counts ranks per chunk), the rank scan down the
 // chunks (and in-block prefixes of the rank totals), pass 2 (forms the bucket
@@ -235,77 +138,16 @@ static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, c
   return 0;
 }
 
-enum class BucketKernel { kStaged, kGeneric, kTwoPass };
-enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16 };
-}  // namespace pdht
-
-// A/B hook points of the choices below (product/pdht_hooks_bucket.h: none
-// taken)
-#include "pdht_hooks_bucket.h"
-
-namespace pdht {
-template <int L, class Out>
-static int launch_two_pass_sel(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
-  // Shapes (waves x keys per lane per sub-tile @ workgroups per CU).  r02's
-  // A/B (8 x 4 / 4 x 16 / 4 x 4 keys, 2-6 WG/CU, per-XCD tile tickets) kept
-  // 4 x 8 @ 4 for both passes.  r04, interleaved, after the fine-plus digit
-  // split had moved work into pass 1 (profiles/r04/ab/bucket_*_tp_shapes*.log):
-  // pass 1 in 8 x 8 @ 2 (4096-key sub-tiles = one counting tile, runs twice as
-  // long, half the barriers per key): 8-B keys at 8192 / 2048 ranks -11 /
-  // -10.5 %, 32-B at 4096 -4 %; 16-B keys gain most with pass 2 in 8 x 8 @ 2
-  // as well (-9 % at 4096 ranks; 8-B keys +4 % with it).  Pass 2 in 8 x 8 @ 3
-  // or 16 x 4 @ 2, pass 1 in 4 x 16 / 16 x 4 / 8 x 4: slower.  Late r05:
-  // 8-B keys into arrays store from one phase (k_bucket_pass2 ONE) and take
-  // pass 2 in 8 x 8 @ 2 as well (4 x 8 @ 4 with ONE: equal to the two-phase
-  // product; 8 x 8 @ 2: -1.0 to -1.3 %, profiles/r05/ab/bucket8k_*.log).
-  if (int rc = hook_two_pass_shape<L, Out>(a, tp, out, st, dev); rc != kNoVariant) return rc;
-  // Late r05: at 8 keys per lane the 16/32-B kernels spilled VGPRs (pass 1
-  // of 32-B keys 78 registers, pass 2 58); in 4 keys per lane none spill
-  // (profiles/r05/ab/bucket_16_32_two_pass_shapes.log, 16M keys): 32-B arrays
-  // at 4096 / 8192 ranks 1.293 -> 0.936 / 1.327 -> 0.978 ms (both passes 8 x 4
-  // @ 2), 32-B records at 8192 ranks 1.728 -> 1.165 and 16-B records at 4096
-  // 0.751 -> 0.656 (pass 2 in 4 x 4 @ 4); 16-B arrays keep 8 x 8 @ 2 (4 keys
-  // per lane +5 %).  8-B records' pass 2 (5 VGPRs spilled at 4 x 8 @ 4) in 8 x
-  // 4 @ 2: 8192 / 2048 ranks 0.389 -> 0.369 / 0.363 -> 0.346 ms.
-  if constexpr (L == 32 && !Out::kPair8)
-    return launch_two_pass<L, Out, 8, 4, 2, 8, 4, 2>(a, tp, out, st, dev);
-  else if constexpr (L >= 16 && Out::kPair8)
-    return launch_two_pass<L, Out, 4, 4, 4, 8, 4, 2>(a, tp, out, st, dev);
-  else if constexpr (L == 16 || (L == 8 && !Out::kPair8))
-    return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
-  else
-    return launch_two_pass<L, Out, 8, 4, 2, 8, 8, 2>(a, tp, out, st, dev);
-}
-
-// Tile-local shapes: pass 1 one tile per sub-tile (8 waves x 8 keys per
-// lane = 4096 keys; 16/32-B keys 8 x 4 = 2048, spill-free) at 2 WG/CU; pass 2
-// the shapes the r02-r05 pass 2 measured best per key size and output kind
-// (launch_two_pass_sel).
-template <int L, class Out>
-static int launch_tl_sel(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
-                         uint64_t *bucket_offsets, hipStream_t st, int dev) {
-  if (int rc = hook_tl_shape<L, Out>(a, tl, out, w, bucket_offsets, st, dev); rc != kNoVariant) return rc;
-  // 16-B keys' pass 2 in 8 x 4 @ 2 (8 x 8 spilled 22 VGPRs: arrays -0.5 /
-  // -3.1 % at 4096 / 2048 ranks, records from 4 x 4 @ 4 -4.9 %,
-  // profiles/r06/ab/bucket_16_tl_pass2_shapes.log)
-  if constexpr ((L == 32 && !Out::kPair8) || L == 16)
-    return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
-  else if constexpr (L == 32)
-    return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
-  else if constexpr (L == 8 && !Out::kPair8)
-    return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
-  else
-    return launch_tl<L, Out, 8, 4, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
-}
-
 // The two digits of rank = c * F + f.  Array outputs of 8/16-B keys take one
 // fine bit more than the balanced split (8192 ranks: F = 256, C = 32): pass 2
 // writes 24 / 32 B per key in runs of ~4096 / C keys against pass 1's 12 / 20 B
 // in runs of ~4096 / F, so longer pass-2 runs pay.  Three boxes, 16M keys
-// (profiles/r03/ab/bucket_two_pass_digits.log): 8 B at 8192 ranks -5.5 /
-// 0 / -3.6 %, 16 B at 4096 ranks -4.3 / -4.0 %, 2048 ranks within +-2 %.
-// 32-B keys (pass 1 writes 36 B/key) lose 3 % with it, and records (AoS
-// rows, pass-2 runs already >= 1 KiB) 1 %: both keep the balanced split.
+// (profiles/r03/ab/bucket_two_pass_digits.log, the r02-r05 form): 8 B at
+// 8192 ranks -5.5 / 0 / -3.6 %, 16 B at 4096 ranks -4.3 / -4.0 %, 2048
+// ranks within +-2 %.  32-B keys (pass 1 writes 36 B/key) lost 3 % with it,
+// and records (AoS rows, pass-2 runs already >= 1 KiB) 1 %: both keep the
+// balanced split (the tile-local form on the balanced split, tuning 164:
+// +2.3 % at 8192 ranks, EXPERIMENTS.md §R6).
 struct Digits {
   u32 fbits, F, C, cbits;
 };
@@ -343,6 +185,80 @@ static void split_segments(u64 nchunks, u64 chunk_keys, u32 F, u64 *SG, u64 *nse
   const u64 step = chunk_keys / F;  // keys of one fine bucket per chunk
   const bool floor_ok = PDHT_TP_EVEN_SEG && (*SG + 1) * step <= 3968 && nchunks - nfl * *SG <= nfl;
   *nsegf = floor_ok ? nfl : (nchunks + *SG - 1) / *SG;
+}
+
+enum class BucketKernel { kStaged, kGeneric, kTwoPass };
+enum class StagedShape { kBallot4x16, kOwner4x16, kOwner8x16 };
+}  // namespace pdht
+
+// A/B hook points of the choices below (product/pdht_hooks_bucket.h: none
+// taken)
+#include "pdht_hooks_bucket.h"
+
+namespace pdht {
+// Sized for the smallest tile any scatter kernel uses, plus the two-pass
+// region when the batch can take that path: 8/16/32-B keys from
+// two_pass_min_ranks() up for the output kind (records: `records`; the tuning
+// build forces two passes at any nranks and always reserves it, at least as
+// large as the r02-r05 form needs: hook_two_pass_region).  16M x 8-B keys at
+// 1024 ranks: 17 MB; from 1536 ranks + 176 MB.
+static BucketWs bucket_layout(void *ws, size_t n, size_t keysize, u32 nranks, bool records) {
+  const u64 ntiles = (n + kBucketMinTile - 1) / kBucketMinTile;
+  const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
+  BucketWs w{};
+  uint8_t *p = static_cast<uint8_t *>(ws);
+  size_t off = 0;
+  w.counts = reinterpret_cast<u32 *>(p + off);
+  off += round256((size_t)nranks * ntiles * 4);
+  w.chunks = reinterpret_cast<u32 *>(p + off);
+  off += round256((size_t)nranks * nchunks * 4);
+  w.totals = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)nranks * 8);
+  w.base = reinterpret_cast<u64 *>(p + off);
+  off += round256((size_t)nranks * 8);
+  w.tickets = reinterpret_cast<u32 *>(p + off);
+  off += 256;
+  const bool two_pass = hook_bucket_reserve(
+      two_pass_keysize(keysize) && nranks >= two_pass_min_ranks(keysize, records), keysize);
+  if (two_pass) {
+    w.region = p + off;
+    size_t q = off;
+    const u32 sh = tl_tile_shift(keysize);
+    const u64 tl_tiles = (n + (1ull << sh) - 1) >> sh;
+    const u64 tl_chunks = (tl_tiles + tl_chunk_tiles(tl_tiles, sh) - 1) / tl_chunk_tiles(tl_tiles, sh);
+    w.tl_starts = reinterpret_cast<uint16_t *>(p + q);
+    q += round256((size_t)tl_tiles * kTpMaxDigits * 2);
+    w.tl_chunkcnt = reinterpret_cast<u32 *>(p + q);
+    q += round256((size_t)tl_chunks * nranks * 4);
+    w.tl_keys = p + q;
+    q += round256(n * keysize);
+    w.tl_lidx = reinterpret_cast<uint16_t *>(p + q);
+    q += round256(n * 2);
+    off = std::max(q, off + hook_two_pass_region((size_t)0, n, keysize, nranks));
+  }
+  w.bytes = off;
+  return w;
+}
+
+// Tile-local shapes: pass 1 one tile per sub-tile (8 waves x 8 keys per
+// lane = 4096 keys; 16/32-B keys 8 x 4 = 2048, spill-free) at 2 WG/CU; pass 2
+// the shapes the r02-r05 pass 2 measured best per key size and output kind
+// (tuning/bucket_two_pass_r05.h launch_two_pass_sel), re-measured in r06.
+template <int L, class Out>
+static int launch_tl_sel(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
+                         uint64_t *bucket_offsets, hipStream_t st, int dev) {
+  if (int rc = hook_tl_shape<L, Out>(a, tl, out, w, bucket_offsets, st, dev); rc != kNoVariant) return rc;
+  // 16-B keys' pass 2 in 8 x 4 @ 2 (8 x 8 spilled 22 VGPRs: arrays -0.5 /
+  // -3.1 % at 4096 / 2048 ranks, records from 4 x 4 @ 4 -4.9 %,
+  // profiles/r06/ab/bucket_16_tl_pass2_shapes.log)
+  if constexpr ((L == 32 && !Out::kPair8) || L == 16)
+    return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 32)
+    return launch_tl<L, Out, 4, 4, 4, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else if constexpr (L == 8 && !Out::kPair8)
+    return launch_tl<L, Out, 8, 8, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
+  else
+    return launch_tl<L, Out, 8, 4, 2, 8, 8, 2>(a, tl, out, w, bucket_offsets, st, dev);
 }
 
 // The tile-local two-pass bucketing (k_bucket_tl_*), n >= 1.
@@ -401,8 +317,8 @@ static StagedShape staged_shape(size_t keysize, u32 nranks) {
 }
 
 // Shared by pdht_bucket_batch_dev (OutSoA) and pdht_bucket_records_dev
-// (OutRec): counting pass, scans, bucket bases, then the scatter into `out`
-// (two passes: bucket_tl).  out_al: alignment bits of the output key rows (0
+// (OutRec): the two passes (bucket_tl), or the counting pass, scans, bucket
+// bases and the scatter into `out`.  out_al: alignment bits of the output key rows (0
 // when they are 8-B aligned 8-B pieces, as in records).
 template <class Out>
 static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nranks, void *workspace,
@@ -435,12 +351,14 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   a.nranks = nranks;
   while ((1u << a.nbits) < nranks) ++a.nbits;
   const size_t hist_lds = (size_t)nranks * 4;
-  // Two passes, tile-local form (r06): no counting pass ahead of pass 1
-  if (kind == BucketKernel::kTwoPass && hook_tile_local(true)) {
-    if (n == 0) {
+  // Two passes: the tile-local form (r06); no counting pass ahead of pass 1
+  // (A/B build: the r02-r05 form under tuning variants 290, 202, 264-272)
+  if (kind == BucketKernel::kTwoPass) {
+    if (int rc = hook_two_pass_r05(a, w, keysize, out, bucket_offsets, st, dev); rc != kNoVariant) {
+      if (rc) return rc;
+    } else if (n == 0) {
       HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
-      k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, 0, nullptr, nullptr,
-                                                nullptr);
+      k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, nullptr);
       g_kernel = "k_bucket_base";
     } else if (int rc = bucket_tl(a, w, keysize, out, bucket_offsets, st, dev)) {
       return rc;
@@ -457,61 +375,12 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   const StagedShape shape = hook_staged_shape(staged_shape<Out>(keysize, nranks));
   const u64 st_tile = shape == StagedShape::kOwner8x16 ? 8192 : kStTile;
   const int waves = nranks <= 4096 ? 8 : 4;  // generic: W x nranks x 4 B of LDS <= 128 KiB
-  const u64 tile = kind == BucketKernel::kTwoPass ? kTpCountTile
-                   : kind == BucketKernel::kStaged ? st_tile
-                                                   : (u64)waves * kScatKPL * 64;
+  const u64 tile = kind == BucketKernel::kStaged ? st_tile : (u64)waves * kScatKPL * 64;
   const u64 ntiles = (n + tile - 1) / tile;
   const u64 nchunks = (ntiles + kBucketChunk - 1) / kBucketChunk;
   a.ts = TileStarts{w.counts, w.chunks, w.base, nranks};
   a.ntiles = ntiles;
-  TwoPass tp{};
-  if (kind == BucketKernel::kTwoPass) {  // the r02-r05 two-pass form (A/B build only)
-    const Digits d = digit_split<Out>(a.nbits, nranks, keysize);
-    tp.fbits = d.fbits;
-    tp.F = d.F;
-    tp.C = d.C;
-    tp.cbits = d.cbits;
-    static_assert(kBucketMaxRanks <= kTpMaxDigits * kTpMaxDigits, "two digits of <= 256 cover every rank");
-    if (tp.F > kTpMaxDigits || tp.C > kTpMaxDigits)  // the kernels' LDS digit tables
-      return fail("two-pass digit split: a digit of %s%lld buckets exceeds the LDS tables", "",
-                  (long long)(tp.F > kTpMaxDigits ? tp.F : tp.C));
-    tp.countsF = w.countsF;
-    tp.chunksF = w.chunksF;
-    tp.totalsF = w.totalsF;
-    tp.chunkcnt = w.chunkcnt;
-    tp.base = w.base;
-    tp.fbase = w.fbase;
-    tp.ikeys = w.ikeys;
-    tp.iidx = w.iidx;
-    tp.ntiles = ntiles;
-    tp.nchunks = (ntiles + kTpChunkTiles - 1) / kTpChunkTiles;
-    split_segments(tp.nchunks, (u64)kTpChunkTiles * kTpCountTile, tp.F, &tp.SG, &tp.nsegf);
-    tp.nseg = (u64)tp.F * tp.nsegf;
-  }
-  if (ntiles && kind == BucketKernel::kTwoPass) {
-    // the count kernel scans the fine counts down each count-chunk itself
-    // (no column-scan launch); A/B 264: the r02-r05 colscan over 32-tile chunks
-    const bool fscan = hook_fscan(true);
-    tp.fchunk = fscan ? kTpChunkTiles : kBucketChunk;
-    const u64 nfchunks = (ntiles + tp.fchunk - 1) / tp.fchunk;
-    u32 *cF = fscan ? w.chunksF : nullptr;
-    const unsigned gc = (unsigned)std::min<u64>(tp.nchunks, (u64)std::max(1, g_dev[dev].cus) * 8);
-    if (keysize == 8)
-      k_bucket_count_tp<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                          ntiles, cF);
-    else if (keysize == 16)
-      k_bucket_count_tp<16><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                           ntiles, cF);
-    else
-      k_bucket_count_tp<32><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, tp.F, w.countsF, w.chunkcnt,
-                                                           ntiles, cF);
-    if (!fscan)
-      k_bucket_colscan<<<dim3((tp.F + 63) / 64, (unsigned)nfchunks), 64, 0, st>>>(w.countsF, ntiles, tp.F,
-                                                                                   w.chunksF);
-    const u32 nbF = (tp.F + 63) / 64;  // both chunk scans in one launch
-    k_bucket_chunkscan2<<<nbF + (nranks + 63) / 64, 64 * kCsWaves, 0, st>>>(
-        w.chunksF, nfchunks, tp.F, w.totalsF, nbF, w.chunkcnt, tp.nchunks, nranks, w.totals);
-  } else if (ntiles) {
+  if (ntiles) {
     const unsigned gc = grid_for(ntiles, 8, dev);
     if (fixed && keysize == 8)
       k_bucket_count_reg<8><<<gc, kBlock, hist_lds, st>>>(a.k, n, a.rk, nranks, w.counts, ntiles, tile);
@@ -529,18 +398,13 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   } else {
     HIP_TRY(hipMemsetAsync(w.totals, 0, (size_t)nranks * 8, st));
   }
-  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, tp.fbits, w.totalsF,
-                                            kind == BucketKernel::kTwoPass ? w.fbase : nullptr, w.tickets);
+  k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, w.tickets);
   g_kernel = "k_bucket_base";
   if (ntiles) {
     int rc = hook_staged_launch(kind == BucketKernel::kStaged, keysize, a, out, st, dev);
     if (rc != kNoVariant) {
       // an A/B alternative ran
-    } else if (kind == BucketKernel::kTwoPass)
-      rc = keysize == 8    ? launch_two_pass_sel<8, Out>(a, tp, out, st, dev)
-           : keysize == 16 ? launch_two_pass_sel<16, Out>(a, tp, out, st, dev)
-                           : launch_two_pass_sel<32, Out>(a, tp, out, st, dev);
-    else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner8x16)
+    } else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner8x16)
       rc = keysize == 8    ? launch_staged<8, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
            : keysize == 16 ? launch_staged<16, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets)
                            : launch_staged<32, Out, false, 8, 16, true, 2>(a, out, st, dev, w.tickets);

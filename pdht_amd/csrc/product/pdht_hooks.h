@@ -22,7 +22,9 @@ static inline int hook_per_cu(int per_cu) { return per_cu; }
 static inline bool hook_zero_copy(bool dflt) { return dflt; }
 // pdht_bucket.hip: reserve the two-pass region in the workspace
 static inline bool hook_bucket_reserve(bool dflt, size_t) { return dflt; }
-// pdht_bucket.hip: log2 keys per pass-1 tile of the tile-local two passes
+// pdht_bucket.hip: log2 keys per pass-1 tile of the tile-local two passes;
+// the fine digit one bit wider for 8/16-B array outputs
 static inline unsigned hook_tl_tile_shift(unsigned dflt, size_t) { return dflt; }
+static inline bool hook_fine_plus(bool dflt) { return dflt; }
 
 }  // namespace pdht

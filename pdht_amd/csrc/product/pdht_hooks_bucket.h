@@ -9,12 +9,11 @@ template <class K>
 static inline K hook_bucket_kind(K dflt, bool, u32) { return dflt; }
 template <class S>
 static inline S hook_staged_shape(S dflt) { return dflt; }
-static inline bool hook_fine_plus(bool dflt) { return dflt; }
-static inline bool hook_fscan(bool dflt) { return dflt; }
-static inline bool hook_tile_local(bool dflt) { return dflt; }
 static inline bool hook_tl_sgmajor(bool dflt) { return dflt; }
-template <int L, class Out, class... A>
-static inline int hook_two_pass_shape(A &&...) { return kNoVariant; }
+// the r02-r05 two passes (the A/B build's baseline): not compiled here
+template <class... A>
+static inline int hook_two_pass_r05(A &&...) { return kNoVariant; }
+static inline size_t hook_two_pass_region(size_t dflt, size_t, size_t, u32) { return dflt; }
 template <int L, class Out, class... A>
 static inline int hook_tl_shape(A &&...) { return kNoVariant; }
 template <class... A>

@@ -31,5 +31,9 @@ static inline unsigned hook_tl_tile_shift(unsigned dflt, size_t keysize) {
   if (v == 302 && keysize == 16) return 12;  // 16-B keys' pass 1 in 4096-key tiles (8 x 8, r06 first form)
   return (v == 294 || v == 295 || v == 297) && keysize <= 16 ? 13 : dflt;
 }
+// 164 / 295: two-pass arrays of 8/16-B keys on the balanced digit split
+static inline bool hook_fine_plus(bool dflt) {
+  return tuning_variant() == 164 || tuning_variant() == 295 ? false : dflt;
+}
 
 }  // namespace pdht

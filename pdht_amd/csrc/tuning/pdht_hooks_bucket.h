@@ -4,16 +4,10 @@
 // variant was measured against the product form (EXPERIMENTS.md).
 #pragma once
 
+#include "bucket_two_pass_r05.h"
+
 namespace pdht {
 
-// The r02-r05 two-pass form (counting kernel + fine counts scanned ahead of
-// pass 1, pass 1 writing global fine-bucket runs) instead of the tile-local
-// one (r06): 290 as r05 shipped it, and its shape variants below.
-static inline bool tuning_two_pass_r05() {
-  const int v = tuning_variant();
-  return v == 290 || v == 202 || v == 264 || (v >= 265 && v <= 272);
-}
-static inline bool hook_tile_local(bool dflt) { return tuning_two_pass_r05() ? false : dflt; }
 // 296 / 297: tile-local pass-2 segments in chunk-range-major order (the
 // workgroups of an XCD gather neighbouring f-runs of the same tiles at once)
 // / 297 the same and the chunk-range-major order on 8192-key tiles (294)
@@ -45,42 +39,7 @@ static inline S hook_staged_shape(S shape) {
   return shape;
 }
 
-// 164: two-pass arrays of 8/16-B keys on the balanced digit split
-static inline bool hook_fine_plus(bool dflt) {
-  return tuning_variant() == 164 || tuning_variant() == 295 ? false : dflt;
-}
-// 264: the r02-r05 fine-count column scan over 32-tile chunks
-static inline bool hook_fscan(bool dflt) { return tuning_variant() == 264 ? false : dflt; }
-
-// Shapes of the r02-r05 two passes.
-template <int L, class Out>
-static int hook_two_pass_shape(const BucketArgs &a, const TwoPass &tp, const Out &out, hipStream_t st, int dev) {
-  // (r04's shape search, tuning 192-201, removed in r05)
-  constexpr int kW = L == 8 && !Out::kPair8 ? 1 : 0;  // (ONE exists for 8-B arrays only)
-  const int v = tuning_variant();
-  if (v == 202)  // r02-r03: 4 x 8 @ 4 both, pass 2 storing in two phases
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, kTpW, kTpKPL, kTpPerCu, false>(a, tp, out, st, dev);
-  if (kW && v == 265)  // r04-r05 product for 8-B arrays: pass 2 two-phase 4 x 8 @ 4
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2, false>(a, tp, out, st, dev);
-  if (kW && v == 266)  // ONE in 4 x 8 @ 4
-    return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
-  if constexpr (L >= 16) {  // r05 spill probe (16/32-B keys in 4 keys per lane) and the r04-r05 shapes
-    switch (v) {
-      case 267: return launch_two_pass<L, Out, 8, 4, 2, 8, 4, 2>(a, tp, out, st, dev);
-      case 268: return launch_two_pass<L, Out, 4, 4, 4, 8, 4, 2>(a, tp, out, st, dev);
-      case 269: return launch_two_pass<L, Out, 8, 4, 2, 4, 8, 4>(a, tp, out, st, dev);
-      case 270:
-        if constexpr (L == 16) return launch_two_pass<L, Out, 8, 8, 2, 8, 8, 2>(a, tp, out, st, dev);
-        else return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
-      default: break;
-    }
-  }
-  if constexpr (L == 8 && Out::kPair8) {  // 8-B records' pass 2: 4 x 4 @ 4 / r04-r05's 4 x 8 @ 4
-    if (v == 271) return launch_two_pass<L, Out, 4, 4, 4, 8, 8, 2>(a, tp, out, st, dev);
-    if (v == 272) return launch_two_pass<L, Out, kTpW, kTpKPL, kTpPerCu, 8, 8, 2>(a, tp, out, st, dev);
-  }
-  return kNoVariant;
-}
+// The r02-r05 two-pass form (290, 202, 264-272): tuning/bucket_two_pass_r05.h
 
 // Shapes of the tile-local two passes (r06).  291: pass 2 in 4 x 8 @ 4;
 // 292: pass 2 in 8 x 4 @ 2; 293: pass 1 in 16 waves (1024 threads) @ 1 on

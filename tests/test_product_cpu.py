@@ -247,20 +247,21 @@ def test_host_wrappers_reject_bad_buffers():
 
 
 def test_bucket_workspace_small_at_low_rank_counts():
-    """The two-pass intermediate (n x (keysize + 4) B) is reserved only at
-    the rank counts that take the two-pass sort."""
+    """The two-pass intermediate (n x (keysize + 2) B: key rows + u16 in-tile
+    indices) is reserved only at the rank counts that take the two-pass sort
+    (ADVICE r02)."""
     n = 16 << 20
     for records, L, thr in ((False, 8, 1536), (False, 16, 1025), (False, 32, 2049),
                             (True, 8, 1536), (True, 16, 1025), (True, 32, 1025)):
         ws = lambda r: P.bucket_workspace_bytes(n, L, r, records=records)  # noqa: E731
         small = ws(1024 if L != 16 else 1000)
         assert small < 64 << 20, (L, small)
-        assert ws(thr) >= small + n * (L + 4)  # either two-pass form fits
-        assert ws(thr - 1) < n * (L + 4)
+        assert ws(thr) >= small + n * (L + 2)
+        assert ws(thr - 1) < n * (L + 2)
         assert ws(8192) >= P.bucket_workspace_bytes(n, L, 8192)
     # ADVICE r05: 32-B array callers at 1025..2048 ranks do not reserve records' intermediate
-    assert P.bucket_workspace_bytes(n, 32, 2048) < n * 36
-    assert P.bucket_workspace_bytes(n, 32, 2048, records=True) >= n * 36
+    assert P.bucket_workspace_bytes(n, 32, 2048) < n * 34
+    assert P.bucket_workspace_bytes(n, 32, 2048, records=True) >= n * 34
     assert P.bucket_workspace_bytes(n, 8, 7) < 1 << 20
     assert P.bucket_workspace_bytes(n, 13, 8192) < n * 17  # generic lengths never take two passes
     assert b"abi 4" in P.lib().pdht_hip_version()
