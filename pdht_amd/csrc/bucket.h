@@ -404,35 +404,6 @@ __device__ __forceinline__ void rank_groups_owner(const Tab &run, u32 wave, cons
   for (int g = 0; g < KPL; ++g) lp[g] = (u32)__shfl((int)base[g], (int)(al[g] >> 8)) + (al[g] & 0xffu);
 }
 
-// rank_groups in batches of B groups, writing each key's index straight into
-// the sorted-order table: B x 2 registers per lane instead of KPL x 3.
-template <int KPL, int B, class Tab>
-__device__ __forceinline__ void rank_and_place(const Tab &run, u32 wave, const u32 (&rr)[KPL], u32 q0, u32 tn,
-                                               u32 nbits, uint16_t *sidx) {
-  const u32 lane = threadIdx.x & 63;
-  const u64 below = (1ull << lane) - 1;
-#pragma unroll
-  for (int g0 = 0; g0 < KPL; g0 += B) {
-    u32 al[B], base[B];  // al = ahead | leader lane << 8
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int g = g0 + b;
-      const bool valid = q0 + g * 64 < tn;
-      const u64 same = same_bucket_lanes(valid, rr[g], nbits);
-      const u32 ahead = (u32)__builtin_popcountll(same & below);
-      al[b] = ahead | ((same ? (u32)__builtin_ctzll(same) : 0u) << 8);
-      base[b] = 0;
-      if (valid && ahead == 0) base[b] = run.add(wave, rr[g], (u32)__builtin_popcountll(same));
-    }
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int g = g0 + b;
-      const u32 lp = (u32)__shfl((int)base[b], (int)(al[b] >> 8)) + (al[b] & 0xffu);
-      if (q0 + g * 64 < tn) sidx[lp] = (uint16_t)(q0 + g * 64);
-    }
-  }
-}
-
 template <int L>
 __device__ __forceinline__ void store_key_row(uint8_t *dst, const RegReader<L / 4> &k) {
   if constexpr (L == 8) {
