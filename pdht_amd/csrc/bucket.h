@@ -808,7 +808,9 @@ struct TwoPassTL {
   u32 ct;                     // tiles per count-chunk
   u64 n, ntiles, nchunks;
   u64 nsegf, nseg;            // segments per fine bucket; segments
-  u32 sgmajor;                // segment order: 0 = f-major (all of f, then f + 1), 1 = chunk-range-major
+  // segment order: blocks of og fine buckets x os segments each, the blocks
+  // f-group-major (og = 1, os = nsegf: all of f, then f + 1)
+  u32 og, os, nsgg;           // nsgg = ceil(nsegf / os)
   uint16_t *startsF;          // [ntiles][F] tile-local first row of fine bucket f
   u32 *chunkcnt;              // [nchunks][nranks] rank histogram of chunk g; after the scan its exclusive prefix
   u32 *inpre, *bsum;          // bucket bases = prefix of bsum[r / 64] + inpre[r] (k_bucket_chunkscan_tl)
@@ -960,8 +962,11 @@ void k_bucket_tl_pass2(FastMod rk, u32 nranks, TwoPassTL tp, Out out) {
   auto coarse = [&](u64 h, u32) { return (u32)rk.mod(h) >> fbits; };
   for (TileOrder o(tp.nseg); o.t < o.end; o.t += o.step) {
     // the count-chunks split evenly over the nsegf segments of f
-    const u32 f = tp.sgmajor ? (u32)(o.t % tp.F) : (u32)(o.t / tp.nsegf);
-    const u64 sg = tp.sgmajor ? o.t / tp.F : o.t % tp.nsegf;
+    const u32 ot = (u32)o.t, gs = tp.og * tp.os;
+    const u32 blk = ot / gs, wi = ot - blk * gs;
+    const u32 f = (blk / tp.nsgg) * tp.og + wi / tp.os;
+    const u64 sg = (u64)(blk % tp.nsgg) * tp.os + wi % tp.os;
+    if (sg >= tp.nsegf) continue;  // (the ragged last block of an f-group; uniform per workgroup)
     const u64 g0 = sg * tp.nchunks / tp.nsegf, g1 = (sg + 1) * tp.nchunks / tp.nsegf;
     const u64 ta = g0 * tp.ct, tb = min(g1 * tp.ct, tp.ntiles);
     // this thread's runs: tiles ta + threadIdx.x * RP + q (contiguous, so a

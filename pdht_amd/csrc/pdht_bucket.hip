@@ -285,8 +285,13 @@ static int bucket_tl(const BucketArgs &a, const BucketWs &w, size_t keysize, con
   const u64 seg_tiles = (tl.nchunks + tl.nsegf - 1) / tl.nsegf * tl.ct;
   if (seg_tiles > kTlMaxRuns)
     return fail("tile-local two-pass: %s%lld tiles per segment exceed the run table", "", (long long)seg_tiles);
-  tl.nseg = (u64)tl.F * tl.nsegf;
-  tl.sgmajor = hook_tl_sgmajor(false);
+  tl.og = 1;
+  tl.os = (u32)tl.nsegf;
+  hook_tl_order(tl.F, tl.nsegf, &tl.og, &tl.os);
+  tl.og = std::min(tl.og, tl.F);  // (powers of two: og divides F)
+  tl.os = std::max(tl.os, 1u);
+  tl.nsgg = (u32)((tl.nsegf + tl.os - 1) / tl.os);
+  tl.nseg = (u64)tl.F * tl.nsgg * tl.os;
   tl.startsF = w.tl_starts;
   tl.chunkcnt = w.tl_chunkcnt;
   tl.inpre = reinterpret_cast<u32 *>(w.base);  // (nranks x u64 of space, unused here: 2 x nranks u32)

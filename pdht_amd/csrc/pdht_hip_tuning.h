@@ -91,6 +91,8 @@ extern "C" {
  *                304  16-B keys' tile-local pass 2 in r06's first shapes (arrays 8x8@2,
  *                     records 4x4@4)
  *                305  32-B records' tile-local pass 2 in 8x4@2
+ *            316-319  tile-local pass-2 segments in blocks of og fine buckets x os
+ *                     segments: 8x8, 16x4, 32x2, 4x16
  *                298  timing probe: tile-local pass 2 reading contiguous rows instead of
  *                     gathering its f-runs (wrong outputs; 8/16-B keys)
  *                302  tile-local, 16-B keys: pass 1 in 8x8 (4096-key tiles; spills 23 VGPRs,

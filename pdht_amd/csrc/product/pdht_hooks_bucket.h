@@ -9,7 +9,7 @@ template <class K>
 static inline K hook_bucket_kind(K dflt, bool, u32) { return dflt; }
 template <class S>
 static inline S hook_staged_shape(S dflt) { return dflt; }
-static inline bool hook_tl_sgmajor(bool dflt) { return dflt; }
+static inline void hook_tl_order(u32, u64, u32 *, u32 *) {}
 // the r02-r05 two passes (the A/B build's baseline): not compiled here
 template <class... A>
 static inline int hook_two_pass_r05(A &&...) { return kNoVariant; }

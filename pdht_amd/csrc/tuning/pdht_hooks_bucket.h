@@ -8,11 +8,18 @@
 
 namespace pdht {
 
-// 296 / 297: tile-local pass-2 segments in chunk-range-major order (the
-// workgroups of an XCD gather neighbouring f-runs of the same tiles at once)
-// / 297 the same and the chunk-range-major order on 8192-key tiles (294)
-static inline bool hook_tl_sgmajor(bool dflt) {
-  return tuning_variant() == 296 || tuning_variant() == 297 ? true : dflt;
+// Tile-local pass-2 segment order, blocks of og fine buckets x os segments
+// (the 64 workgroups of an XCD run one block at a time): 296 / 297
+// chunk-range-major (og = F, os = 1; 297 on 8192-key tiles, 294); 316-319
+// og x os = 8 x 8, 16 x 4, 32 x 2, 4 x 16 (neighbouring f-runs of the same
+// tiles gathered together, each bucket's neighbouring runs stored together).
+static inline void hook_tl_order(u32 F, u64, u32 *og, u32 *os) {
+  const int v = tuning_variant();
+  if (v == 296 || v == 297) *og = F, *os = 1;
+  if (v == 316) *og = 8, *os = 8;
+  if (v == 317) *og = 16, *os = 4;
+  if (v == 318) *og = 32, *os = 2;
+  if (v == 319) *og = 4, *os = 16;
 }
 
 // 21: the generic-length kernel for 8/16/32-B keys too; 70: one pass (the
