@@ -929,7 +929,13 @@ void k_bucket_tl_pass1(const uint8_t *__restrict__ keys, FastMod rk, u32 nranks,
 // PROBE (A/B timing only, wrong outputs): 1 = every sub-tile reads its rows
 // contiguously from row o.t * 3840 instead of through the row map (what the
 // gather costs).
-template <int L, class Out, int W, int KPL, int WPE, bool ONE = (L == 8 && !Out::kPair8), int PROBE = 0>
+// NTG: the gather's loads non-temporal.  Plain loads keep the lines a
+// neighbouring f-run shares in L2 for the segment that reads it next:
+// 8-B keys at 8192 / 2048 ranks -3.9 / -1.5 %, 16-B keys -5.7 %, 8-B
+// records -4.4 %, 32-B keys equal; 32-B records +2.5 % and keep nt
+// (profiles/r06/ab/bucket_tl_gather_temporal.log).
+template <int L, class Out, int W, int KPL, int WPE, bool ONE = (L == 8 && !Out::kPair8), int PROBE = 0,
+          bool NTG = (L == 32 && Out::kPair8)>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_bucket_tl_pass2(FastMod rk, u32 nranks, TwoPassTL tp, Out out) {
   static_assert(!ONE || (L == 8 && !Out::kPair8), "one store phase: 8-B keys into arrays");
@@ -1016,8 +1022,8 @@ void k_bucket_tl_pass2(FastMod rk, u32 nranks, TwoPassTL tp, Out out) {
       for (int k = 0; k < KPL; ++k) {
         const u32 row = PROBE == 1 ? (u32)((o.t * 3840 + k0 + min(q0 + k * 64, tn - 1)) % tp.n)
                                    : sidx[min(q0 + k * 64, tn - 1)];
-        load_key_regs<L, true>(tp.ikeys, row, kr[k]);
-        ix[k] = (row & ~tmask) | (u32)__builtin_nontemporal_load(tp.ilidx + row);
+        load_key_regs<L, NTG>(tp.ikeys, row, kr[k]);
+        ix[k] = (row & ~tmask) | (u32)(NTG ? __builtin_nontemporal_load(tp.ilidx + row) : tp.ilidx[row]);
       }
       u64 h[ONE ? 1 : KPL];
       u32 cc[KPL];

@@ -91,6 +91,8 @@ extern "C" {
  *                304  16-B keys' tile-local pass 2 in r06's first shapes (arrays 8x8@2,
  *                     records 4x4@4)
  *                305  32-B records' tile-local pass 2 in 8x4@2
+ *                320  tile-local pass 2's gather in the other load policy (non-temporal;
+ *                     32-B records temporal)
  *            316-319  tile-local pass-2 segments in blocks of og fine buckets x os
  *                     segments: 8x8, 16x4, 32x2, 4x16
  *                298  timing probe: tile-local pass 2 reading contiguous rows instead of

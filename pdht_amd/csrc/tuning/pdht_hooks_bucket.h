@@ -82,6 +82,16 @@ static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &ou
     if (v == 294 || v == 295 || v == 297)
       return launch_tl<L, Out, 8, 8, 2, 16, 8, 1>(a, tl, out, w, bucket_offsets, st, dev);
   }
+  if (v == 320) {  // the product's shapes, pass 2 gathering with non-temporal loads (r06 before the switch)
+    if constexpr (L == 8 && !Out::kPair8)
+      return launch_tl<L, Out, 8, 8, 2, 8, 8, 2, 0, true>(a, tl, out, w, bucket_offsets, st, dev);
+    else if constexpr (L == 8)
+      return launch_tl<L, Out, 8, 4, 2, 8, 8, 2, 0, true>(a, tl, out, w, bucket_offsets, st, dev);
+    else if constexpr (L == 32 && Out::kPair8)
+      return launch_tl<L, Out, 4, 4, 4, 8, 4, 2, 0, false>(a, tl, out, w, bucket_offsets, st, dev);
+    else
+      return launch_tl<L, Out, 8, 4, 2, 8, 4, 2, 0, true>(a, tl, out, w, bucket_offsets, st, dev);
+  }
   if constexpr (L == 32 && Out::kPair8)
     if (v == 305)  // 32-B records' pass 2 in 8 x 4 @ 2 (the arrays' shape)
       return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
