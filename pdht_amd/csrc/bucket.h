@@ -639,12 +639,16 @@ struct XcdTickets {
   }
 };
 
+// NTK: the keys loaded non-temporally.  Plain loads measured faster (r06,
+// profiles/r06/ab/bucket_staged_key_loads.log: 1024 ranks 8-B keys -1.9 %,
+// 8-B records -4.1 %, 16-B -1.9 %, 32-B -12 %).
 // DYN: tiles handed out by a per-XCD ticket (one vector atomic per tile)
 // instead of the static stride of TileOrder, so the tiles in flight on an XCD
 // stay one contiguous window however the workgroups drift: the runs of one
 // bucket from neighbouring tiles are written close in time and leave L2 as
 // whole lines.
-template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false, bool DYN = false, int OB = 0>
+template <int L, class Out, int W = kStW, int KPL = kStKPL, bool PACK = false, bool DYN = false, int OB = 0,
+          bool NTK = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(PACK ? 3 : (L == 8 || W == 8) ? 2 : 1)))
 void k_bucket_scatter_staged(
     const uint8_t *__restrict__ keys, u64 n, FastMod rk, u32 nranks, u32 nbits, TileStarts ts, u64 ntiles,
@@ -675,7 +679,7 @@ void k_bucket_scatter_staged(
     const u32 q0 = wave * kSub + lane;
     RegReader<L / 4> kr[KPL];
 #pragma unroll
-    for (int g = 0; g < KPL; ++g) load_key_regs<L, true>(keys, min(tbase + q0 + g * 64, n - 1), kr[g]);
+    for (int g = 0; g < KPL; ++g) load_key_regs<L, NTK>(keys, min(tbase + q0 + g * 64, n - 1), kr[g]);
     u64 h[KPL];
     u32 rr[KPL];
 #pragma unroll
@@ -830,7 +834,7 @@ constexpr size_t tl_pass1_lds_bytes(u32 nranks) {
 template <int W, int KPL>
 constexpr size_t tl_pass2_lds_bytes() { return (size_t)W * KPL * 64 * (8 + 4); }
 
-template <int L, int W, int KPL, int WPE>
+template <int L, int W, int KPL, int WPE, bool NTK = true>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_bucket_tl_pass1(const uint8_t *__restrict__ keys, FastMod rk, u32 nranks, TwoPassTL tp) {
   constexpr u32 kTile = W * KPL * 64, kB = W * 64, kSub = KPL * 64;
@@ -858,7 +862,7 @@ void k_bucket_tl_pass1(const uint8_t *__restrict__ keys, FastMod rk, u32 nranks,
       for (u32 j = threadIdx.x; j < W * tp.F; j += kB) runt[j] = 0;
       RegReader<L / 4> kr[KPL];
 #pragma unroll
-      for (int k = 0; k < KPL; ++k) load_key_regs<L, true>(keys, min(tbase + q0 + k * 64, n - 1), kr[k]);
+      for (int k = 0; k < KPL; ++k) load_key_regs<L, NTK>(keys, min(tbase + q0 + k * 64, n - 1), kr[k]);
       u32 ff[KPL];
 #pragma unroll
       for (int k = 0; k < KPL; ++k) {

@@ -63,7 +63,8 @@ struct BucketArgs {
   u64 ntiles;
 };
 
-template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL, bool DYN = false, int OB = 0>
+template <int L, class Out, bool PACK = false, int W = kStW, int KPL = kStKPL, bool DYN = false, int OB = 0,
+          bool NTK = false>
 static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, int dev, u32 *tickets = nullptr) {
   static const char *const names[3] = {"k_bucket_scatter_staged<8B>", "k_bucket_scatter_staged<16B>",
                                        "k_bucket_scatter_staged<32B>"};
@@ -76,7 +77,7 @@ static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, in
                                          "k_bucket_scatter_staged<32B,own,8x16>"};
   g_kernel = (OB ? (W == 8 ? o8names : onames) : PACK ? pnames : names)[L == 8 ? 0 : L == 16 ? 1 : 2];
   const size_t bytes = staged_lds_bytes(a.nranks, W, KPL, PACK, OB);
-  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN, OB>;
+  auto fn = &k_bucket_scatter_staged<L, Out, W, KPL, PACK, DYN, OB, NTK>;
   if (int rc = set_lds(reinterpret_cast<const void *>(fn), bytes)) return rc;
   const int per_cu = bytes <= 53 * 1024 ? 3 : bytes <= 80 * 1024 ? 2 : 1;
   unsigned g = (unsigned)std::min<u64>(a.ntiles, (u64)std::max(1, g_dev[dev].cus) * per_cu);
@@ -86,7 +87,7 @@ static int launch_staged(const BucketArgs &a, const Out &out, hipStream_t st, in
   if (DYN && g % 8 == 0)
     fn<<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, tickets);
   else
-    k_bucket_scatter_staged<L, Out, W, KPL, PACK, false, OB>
+    k_bucket_scatter_staged<L, Out, W, KPL, PACK, false, OB, NTK>
         <<<g, W * 64, bytes, st>>>(a.k, a.n, a.rk, a.nranks, a.nbits, a.ts, a.ntiles, out, nullptr);
   return 0;
 }
@@ -113,7 +114,7 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
 // by c, stores at the final slots).  Pass 1 in W1 x KPL1 (one tile) @ PER_CU1,
 // pass 2 in W x KPL @ PER_CU.
 template <int L, class Out, int W, int KPL, int PER_CU, int W1, int KPL1, int PER_CU1, int PROBE = 0,
-          bool NTG = (L == 32 && Out::kPair8)>
+          bool NTG = (L == 32 && Out::kPair8), bool NTK1 = true>
 static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
                      uint64_t *bucket_offsets, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_tl_pass2<8B>", "k_bucket_tl_pass2<16B>",
@@ -122,7 +123,7 @@ static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, c
   constexpr int WPE = PER_CU * W / 4 > 8 ? 8 : PER_CU * W / 4;
   constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;
   const size_t b1 = tl_pass1_lds_bytes<W1, KPL1>(a.nranks), b2 = tl_pass2_lds_bytes<W, KPL>();
-  auto f1 = &k_bucket_tl_pass1<L, W1, KPL1, WPE1>;
+  auto f1 = &k_bucket_tl_pass1<L, W1, KPL1, WPE1, NTK1>;
   auto f2 = &k_bucket_tl_pass2<L, Out, W, KPL, WPE, (L == 8 && !Out::kPair8), PROBE, NTG>;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
@@ -407,7 +408,7 @@ static int bucket_impl(const void *keys, size_t keysize, size_t n, uint32_t nran
   k_bucket_base<<<1, kBaseThreads, 0, st>>>(w.totals, nranks, w.base, bucket_offsets, w.tickets);
   g_kernel = "k_bucket_base";
   if (ntiles) {
-    int rc = hook_staged_launch(kind == BucketKernel::kStaged, keysize, a, out, st, dev);
+    int rc = hook_staged_launch(kind == BucketKernel::kStaged, keysize, a, out, st, dev, shape, w.tickets);
     if (rc != kNoVariant) {
       // an A/B alternative ran
     } else if (kind == BucketKernel::kStaged && shape == StagedShape::kOwner8x16)

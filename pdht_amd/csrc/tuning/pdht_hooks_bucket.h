@@ -92,6 +92,17 @@ static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &ou
     else
       return launch_tl<L, Out, 8, 4, 2, 8, 4, 2, 0, true>(a, tl, out, w, bucket_offsets, st, dev);
   }
+  if (v == 322) {  // the product's shapes, pass 1 loading its keys with plain (temporal) loads
+    constexpr bool NG = L == 32 && Out::kPair8;
+    if constexpr (L == 8 && !Out::kPair8)
+      return launch_tl<L, Out, 8, 8, 2, 8, 8, 2, 0, NG, false>(a, tl, out, w, bucket_offsets, st, dev);
+    else if constexpr (L == 8)
+      return launch_tl<L, Out, 8, 4, 2, 8, 8, 2, 0, NG, false>(a, tl, out, w, bucket_offsets, st, dev);
+    else if constexpr (L == 32 && Out::kPair8)
+      return launch_tl<L, Out, 4, 4, 4, 8, 4, 2, 0, NG, false>(a, tl, out, w, bucket_offsets, st, dev);
+    else
+      return launch_tl<L, Out, 8, 4, 2, 8, 4, 2, 0, NG, false>(a, tl, out, w, bucket_offsets, st, dev);
+  }
   if constexpr (L == 32 && Out::kPair8)
     if (v == 305)  // 32-B records' pass 2 in 8 x 4 @ 2 (the arrays' shape)
       return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);
@@ -100,13 +111,29 @@ static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &ou
 
 // 85: the staged scatter in the static tile order (the r02 default before the
 // per-XCD tickets)
-template <class Out>
+template <class Out, class S>
 static int hook_staged_launch(bool staged, size_t keysize, const BucketArgs &a, const Out &out, hipStream_t st,
-                              int dev) {
-  if (!staged || tuning_variant() != 85) return kNoVariant;
-  return keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
-         : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
-                         : launch_staged<32, Out>(a, out, st, dev);
+                              int dev, S shape, u32 *tickets) {
+  if (!staged) return kNoVariant;
+  const int v = tuning_variant();
+  if (v == 85)
+    return keysize == 8    ? launch_staged<8, Out>(a, out, st, dev)
+           : keysize == 16 ? launch_staged<16, Out>(a, out, st, dev)
+                           : launch_staged<32, Out>(a, out, st, dev);
+  if (v == 321) {  // the product's shapes, keys loaded non-temporally (r02-r06 before the switch)
+    if (shape == S::kOwner8x16)
+      return keysize == 8    ? launch_staged<8, Out, false, 8, 16, true, 2, true>(a, out, st, dev, tickets)
+             : keysize == 16 ? launch_staged<16, Out, false, 8, 16, true, 2, true>(a, out, st, dev, tickets)
+                             : launch_staged<32, Out, false, 8, 16, true, 2, true>(a, out, st, dev, tickets);
+    if (shape == S::kOwner4x16)
+      return keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 2, true>(a, out, st, dev, tickets)
+             : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 2, true>(a, out, st, dev, tickets)
+                             : launch_staged<32, Out, false, kStW, kStKPL, true, 2, true>(a, out, st, dev, tickets);
+    return keysize == 8    ? launch_staged<8, Out, false, kStW, kStKPL, true, 0, true>(a, out, st, dev, tickets)
+           : keysize == 16 ? launch_staged<16, Out, false, kStW, kStKPL, true, 0, true>(a, out, st, dev, tickets)
+                           : launch_staged<32, Out, false, kStW, kStKPL, true, 0, true>(a, out, st, dev, tickets);
+  }
+  return kNoVariant;
 }
 
 // 112: the r02 record store order (header halves first, {mbits, key} halves

@@ -571,6 +571,8 @@ BUCKET_CASES += [(L, nr, n, 0) for (L, nr) in ((8, 1536), (8, 2047), (16, 1025),
 BUCKET_CASES += [(L, nr, n, 21) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192) for n in (4095, 300007)]
 BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2048, 2049, 8192)
                  for n in (1, 4095, 300007, (1 << 20) + 5)]
+# 321: the staged scatter loading its keys non-temporally (the r02-r06 policy)
+BUCKET_CASES += [(L, nr, n, 321) for L in (8, 16, 32) for nr in (7, 600, 1000, 1535) for n in (4097, 300007)]
 BUCKET_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (1, 7, 1000, 1535)
                  for n in (1, 4095, 300007, (1 << 20) + 5, (16 << 20) + 3)]
 BUCKET_CASES += [(L, nr, n, v) for v in (83, 87, 89) for L in (8, 16, 32)
@@ -601,7 +603,7 @@ BUCKET_CASES += [(L, nr, n, 0) for L in (8, 16) for nr in (8192,) for n in ((1 <
 BUCKET_CASES += [(L, nr, n, 0) for L in (8, 32) for nr in (2049, 8192) for n in ((4 << 20) + 7, (8 << 20) + 4097)]
 # 290: the r02-r05 two-pass form (counting kernel ahead of pass 1, global fine-bucket runs);
 # 291-293: tile-local shapes (pass 2 in 4 x 8 @ 4 / 8 x 4 @ 2; pass 1 in 16 waves @ 1)
-BUCKET_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320) for L in (8, 16, 32) for nr in (2049, 8192)
+BUCKET_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320, 322) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
 
 
@@ -713,6 +715,7 @@ RECORD_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 7, 1000
                 for n in (0, 1, 4095, 100003)]
 RECORD_CASES += [(L, nr, n, v) for v in (21, 70, 71) for L in (8, 16, 32) for nr in (7, 1000, 2048, 8192)
                  for n in (4097, 300007)]
+RECORD_CASES += [(L, nr, n, 321) for L in (8, 16, 32) for nr in (7, 600, 1000) for n in (4097, 300007)]
 RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n in (4097, (2 << 20) + 9)]
 # records switch to owner-table ranking for 16/32-B keys from 512 ranks while
 # two workgroups fit a CU (staged_shape): both edges of both thresholds
@@ -726,7 +729,7 @@ RECORD_CASES += [(8, nr, n, v) for v in (271, 272) for nr in (2049, 8192) for n 
 # 112: the r02 store order of 8-B records (header halves a staging round early)
 RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
 # r06: records on the r02-r05 two-pass form (290) and the tile-local shapes 291-293
-RECORD_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320) for L in (8, 16, 32) for nr in (2049, 8192)
+RECORD_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320, 322) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (4097, 300007)]
 RECORD_CASES += [(L, 8192, (4 << 20) + 7, 0) for L in (8, 32)]
 
