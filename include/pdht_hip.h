@@ -123,7 +123,7 @@ int pdht_place_batch_dev(const void *keys, size_t keysize, size_t n,
  * ptindex_out is best NULL.  nranks <= 8192, n < 2^32.  `workspace`
  * (device) must hold pdht_bucket_workspace_bytes(n, keysize, nranks): the
  * per-tile counts and, for 8/16/32-B keys at the rank counts that take the
- * two-pass sort (from 1536 / 1025 / 2049 ranks for 8 / 16 / 32-B keys), its
+ * two-pass sort (from 1575 / 1575 / 2049 ranks for 8 / 16 / 32-B keys), its
  * intermediate (about n x (keysize + 2) bytes). */
 size_t pdht_bucket_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
@@ -152,8 +152,8 @@ int pdht_bucket_batch_dev(const void *keys, size_t keysize, size_t n,
  * mbits % nptes; the MPI message carries ht_index instead). */
 size_t pdht_bucket_record_bytes(size_t keysize);
 /* Workspace of pdht_bucket_records_dev: as pdht_bucket_workspace_bytes, with
- * the records' two-pass thresholds (32-B keys from 1025 ranks instead of
- * 2049); never smaller than the array query. */
+ * the records' two-pass thresholds (from 2048 / 1463 / 256 ranks for 8 / 16 /
+ * 32-B keys). */
 size_t pdht_bucket_records_workspace_bytes(size_t n, size_t keysize, uint32_t nranks);
 int pdht_bucket_records_dev(const void *keys, size_t keysize, size_t n,
                             uint32_t nranks, uint32_t msg_type, uint32_t src_rank,

@@ -609,6 +609,7 @@ __device__ __forceinline__ void staged_store(u64 *stage, const u32 *delta, u32 t
 // 8-B keys, 1024 ranks.
 constexpr int kStW = 4, kStKPL = 16;
 constexpr u32 kStTile = kStW * kStKPL * 64;
+constexpr size_t kStagedStaticLds = 64;  // >= the staged kernels' static __shared__ bytes (<= 40)
 constexpr size_t staged_lds_bytes(u32 nranks, int W = kStW, int KPL = kStKPL, bool PACK = false, int OB = 0) {
   return (size_t)W * KPL * 64 * 10 + (PACK ? (size_t)W * ((nranks + 1) & ~1u) * 2 : (size_t)W * nranks * 4) +
          (size_t)nranks * 4 + (size_t)W * OB * nranks;

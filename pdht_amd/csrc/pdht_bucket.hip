@@ -23,16 +23,22 @@ struct BucketWs {
 };
 static size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
 static bool two_pass_keysize(size_t keysize) { return keysize == 8 || keysize == 16 || keysize == 32; }
-// Two-pass bucketing from this many ranks up (interleaved
-// A/B on 16M keys; at 1024 ranks one pass is 10 % faster for 8-B keys, equal
-// for 16-B keys, 30 % faster for 32-B keys; at 2048 ranks two passes are 1.3x
-// faster for 8-B keys and at 8192 ranks 2.1x).  Late r05, with the 32-B
-// passes no longer spilling: 32-B records take two passes from 1025 ranks
-// (1024 ranks -3 %, 2048 ranks -13 %), 32-B arrays still from 2049 (one
-// pass 0.82 / 0.95 ms against two 0.95 / 0.99 at 1024 / 2048 ranks,
-// profiles/r05/ab/bucket_16_32_two_pass_shapes.log).
+// Two-pass bucketing from this many ranks up.  The one-pass staged scatter
+// wins while its owner-table shapes fit (staged_shape): arrays of 8/16-B keys
+// on 8 x 16 tiles up to 1574 ranks, 16-B records on 4 x 16 tiles up to 1462,
+// 8-B records (ballots at two workgroups per CU) up to 2047; past those the
+// tile-local two passes win (r06, both forms re-measured after their r06
+// load-policy changes, profiles/r06/ab/bucket_two_pass_thresholds.log: 8-B
+// arrays at 1536 ranks 0.269 one pass / 0.309 two, at 2048 0.463 / 0.294;
+// 16-B arrays at 1025 / 1536 0.385 / 0.411 against 0.426 / 0.430, at 1576
+// 0.540 / 0.441; 8-B records at 1536-1792 0.308-0.313 / 0.332-0.335, at
+// 2048 0.472 / 0.325; 16-B records at 1462 0.547 / 0.575, at 1536 0.592 /
+// 0.582).  32-B arrays stay one pass to 2048 (0.838 / 0.906 at 2048); 32-B
+// records take two passes from 256 ranks (256 / 512 / 1024: 1.071 / 1.067 /
+// 1.093 against 1.111 / 1.130 / 1.166; below 256 not measured).
 static u32 two_pass_min_ranks(size_t keysize, bool records) {
-  return keysize == 8 ? 1536 : keysize == 16 ? 1025 : records ? 1025 : 2049;
+  if (records) return keysize == 8 ? 2048 : keysize == 16 ? 1463 : 256;
+  return keysize == 32 ? 2049 : 1575;
 }
 // Tile-local two-pass sort (r06, bucket.h k_bucket_tl_*): pass-1 tiles of
 // 4096 keys for 8-B keys, 2048 for 16/32-B keys (8 waves x 4 keys per lane,
@@ -318,7 +324,9 @@ static StagedShape staged_shape(size_t keysize, u32 nranks) {
     if (staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024) return StagedShape::kOwner4x16;
     return StagedShape::kBallot4x16;
   }
-  if (keysize != 32 && staged_lds_bytes(nranks, 8, 16, false, 2) <= 160 * 1024) return StagedShape::kOwner8x16;
+  // (kStagedStaticLds: the kernels' own __shared__ words, 40 B, on top)
+  if (keysize != 32 && staged_lds_bytes(nranks, 8, 16, false, 2) + kStagedStaticLds <= 160 * 1024)
+    return StagedShape::kOwner8x16;
   if (staged_lds_bytes(nranks, kStW, kStKPL, false, 2) <= 80 * 1024) return StagedShape::kOwner4x16;
   return StagedShape::kBallot4x16;
 }

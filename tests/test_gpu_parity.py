@@ -565,8 +565,9 @@ def test_device_wrappers_validate_outputs(dev):
 BUCKET_CASES = [(L, nr, n, 0) for L in (8, 13, 16, 32, 64) for nr in (1, 2, 7, 1000, 4096, 4097, 8192)
                 for n in (0, 1, 4095, 100003)]
 # the product's two-pass entry points with the fine-plus digit split:
-# 8-B keys from 1536 ranks (nbits 11: F = 128, C = 12 at 1536), 16-B keys from 1025
-BUCKET_CASES += [(L, nr, n, 0) for (L, nr) in ((8, 1536), (8, 2047), (16, 1025), (16, 2048))
+# arrays: 8/16-B keys from 1575 ranks (the last 8 x 16 owner shape at 1574), 32-B from 2049
+BUCKET_CASES += [(L, nr, n, 0) for (L, nr) in ((8, 1536), (8, 1574), (8, 1575), (8, 2047), (16, 1025), (16, 1574),
+                                                (16, 1575), (16, 2048))
                  for n in (4095, 300007)]
 BUCKET_CASES += [(L, nr, n, 21) for L in (8, 16, 32) for nr in (7, 1000, 2049, 8192) for n in (4095, 300007)]
 BUCKET_CASES += [(L, nr, n, v) for v in (70, 71) for L in (8, 16, 32) for nr in (2, 7, 64, 1000, 2048, 2049, 8192)
@@ -609,7 +610,8 @@ BUCKET_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316,
 
 def _bucket_kernel(L, nranks, variant, records=False):
     """Product: the staged scatter for 8/16/32-B keys below the two-pass
-    threshold (1536 / 1025 / 2049 ranks), two passes from it, the generic
+    threshold (arrays 1575 / 1575 / 2049 ranks, records 2048 / 1463 / 256 for
+    8 / 16 / 32-B keys), two passes from it, the generic
     kernel for other lengths.  Tuning variants: 21 forces the generic-length
     kernel, 70 one pass up to 2048 ranks, 71 two passes from 2 ranks up, 85
     the staged scatter in the static tile order instead of per-XCD tickets,
@@ -619,7 +621,7 @@ def _bucket_kernel(L, nranks, variant, records=False):
     if variant == 21:
         return wg
     if L in (8, 16, 32):
-        two_pass_from = {8: 1536, 16: 1025, 32: 1025 if records else 2049}[L]
+        two_pass_from = ({8: 2048, 16: 1463, 32: 256} if records else {8: 1575, 16: 1575, 32: 2049})[L]
         one_pass = variant == 70 and nranks <= 2048
         if (variant == 71 and nranks >= 2) or (not one_pass and nranks >= two_pass_from):
             # the tile-local form (r06); the r02-r05 form under 290 and its shape variants
@@ -635,7 +637,7 @@ def _bucket_kernel(L, nranks, variant, records=False):
             return f"k_bucket_scatter_staged<{L}B,own>"
         if variant in (85, 89) or records or nranks < 512:
             return f"k_bucket_scatter_staged<{L}B>"
-        if L != 32 and 81920 + 52 * nranks <= 160 * 1024:
+        if L != 32 and 81920 + 52 * nranks + 64 <= 160 * 1024:
             return f"k_bucket_scatter_staged<{L}B,own,8x16>"
         if 40960 + 28 * nranks <= 80 * 1024:
             return f"k_bucket_scatter_staged<{L}B,own>"
@@ -720,8 +722,10 @@ RECORD_CASES += [(L, nr, n, 85) for L in (8, 16, 32) for nr in (7, 1000) for n i
 # records switch to owner-table ranking for 16/32-B keys from 512 ranks while
 # two workgroups fit a CU (staged_shape): both edges of both thresholds
 RECORD_CASES += [(L, nr, 300007, 0) for L in (8, 16, 32) for nr in (511, 512, 1462, 1463)]
-# 32-B records take two passes from 1025 ranks (arrays from 2049)
-RECORD_CASES += [(32, nr, n, 0) for nr in (1024, 1025, 2048) for n in (4097, 300007)]
+# records take two passes from 2048 / 1463 / 256 ranks (8 / 16 / 32-B keys)
+RECORD_CASES += [(32, nr, n, 0) for nr in (255, 256, 1024, 1025, 2048) for n in (4097, 300007)]
+RECORD_CASES += [(L, nr, n, 0) for (L, nr) in ((8, 1536), (8, 2047), (8, 2048), (16, 1462), (16, 1463))
+                 for n in (4097, 300007)]
 # two-pass shapes of records: 267-270 (16/32-B keys), 271 / 272 (8-B keys' pass 2 in 4 keys per lane)
 RECORD_CASES += [(L, nr, n, v) for v in (267, 268, 269, 270) for L in (16, 32) for nr in (2049, 8192)
                  for n in (4097, 300007)]

@@ -251,10 +251,10 @@ def test_bucket_workspace_small_at_low_rank_counts():
     indices) is reserved only at the rank counts that take the two-pass sort
     (ADVICE r02)."""
     n = 16 << 20
-    for records, L, thr in ((False, 8, 1536), (False, 16, 1025), (False, 32, 2049),
-                            (True, 8, 1536), (True, 16, 1025), (True, 32, 1025)):
+    for records, L, thr in ((False, 8, 1575), (False, 16, 1575), (False, 32, 2049),
+                            (True, 8, 2048), (True, 16, 1463), (True, 32, 256)):
         ws = lambda r: P.bucket_workspace_bytes(n, L, r, records=records)  # noqa: E731
-        small = ws(1024 if L != 16 else 1000)
+        small = ws(min(thr - 1, 1000))
         assert small < 64 << 20, (L, small)
         assert ws(thr) >= small + n * (L + 2)
         assert ws(thr - 1) < n * (L + 2)
