@@ -120,7 +120,7 @@ static int launch_wg(const BucketArgs &a, const Out &out, u32 L, hipStream_t st,
 // by c, stores at the final slots).  Pass 1 in W1 x KPL1 (one tile) @ PER_CU1,
 // pass 2 in W x KPL @ PER_CU.
 template <int L, class Out, int W, int KPL, int PER_CU, int W1, int KPL1, int PER_CU1, int PROBE = 0,
-          bool NTG = (L == 32 && Out::kPair8), bool NTK1 = true>
+          bool NTG = (L == 32 && Out::kPair8), bool NTK1 = true, bool ONE = (L == 8 && !Out::kPair8)>
 static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, const BucketWs &w,
                      uint64_t *bucket_offsets, hipStream_t st, int dev) {
   static const char *const names[3] = {"k_bucket_tl_pass2<8B>", "k_bucket_tl_pass2<16B>",
@@ -130,7 +130,7 @@ static int launch_tl(const BucketArgs &a, const TwoPassTL &tl, const Out &out, c
   constexpr int WPE1 = PER_CU1 * W1 / 4 > 8 ? 8 : PER_CU1 * W1 / 4;
   const size_t b1 = tl_pass1_lds_bytes<W1, KPL1>(a.nranks), b2 = tl_pass2_lds_bytes<W, KPL>();
   auto f1 = &k_bucket_tl_pass1<L, W1, KPL1, WPE1, NTK1>;
-  auto f2 = &k_bucket_tl_pass2<L, Out, W, KPL, WPE, (L == 8 && !Out::kPair8), PROBE, NTG>;
+  auto f2 = &k_bucket_tl_pass2<L, Out, W, KPL, WPE, ONE, PROBE, NTG>;
   if (int rc = set_lds(reinterpret_cast<const void *>(f1), b1)) return rc;
   if (int rc = set_lds(reinterpret_cast<const void *>(f2), b2)) return rc;
   const u64 cus = (u64)std::max(1, g_dev[dev].cus);

@@ -91,6 +91,7 @@ extern "C" {
  *                304  16-B keys' tile-local pass 2 in r06's first shapes (arrays 8x8@2,
  *                     records 4x4@4)
  *                305  32-B records' tile-local pass 2 in 8x4@2
+ *                323  8-B arrays' tile-local pass 2 storing in two phases (not ONE)
  *                322  tile-local pass 1 loading its keys with plain (temporal) loads
  *                321  the staged scatter loading its keys non-temporally (before r06)
  *                320  tile-local pass 2's gather in the other load policy (non-temporal;

@@ -103,6 +103,9 @@ static int hook_tl_shape(const BucketArgs &a, const TwoPassTL &tl, const Out &ou
     else
       return launch_tl<L, Out, 8, 4, 2, 8, 4, 2, 0, NG, false>(a, tl, out, w, bucket_offsets, st, dev);
   }
+  if constexpr (L == 8 && !Out::kPair8)
+    if (v == 323)  // 8-B arrays' pass 2 storing in two phases (metadata, then the keys)
+      return launch_tl<L, Out, 8, 8, 2, 8, 8, 2, 0, false, true, false>(a, tl, out, w, bucket_offsets, st, dev);
   if constexpr (L == 32 && Out::kPair8)
     if (v == 305)  // 32-B records' pass 2 in 8 x 4 @ 2 (the arrays' shape)
       return launch_tl<L, Out, 8, 4, 2, 8, 4, 2>(a, tl, out, w, bucket_offsets, st, dev);

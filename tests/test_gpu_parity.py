@@ -604,7 +604,7 @@ BUCKET_CASES += [(L, nr, n, 0) for L in (8, 16) for nr in (8192,) for n in ((1 <
 BUCKET_CASES += [(L, nr, n, 0) for L in (8, 32) for nr in (2049, 8192) for n in ((4 << 20) + 7, (8 << 20) + 4097)]
 # 290: the r02-r05 two-pass form (counting kernel ahead of pass 1, global fine-bucket runs);
 # 291-293: tile-local shapes (pass 2 in 4 x 8 @ 4 / 8 x 4 @ 2; pass 1 in 16 waves @ 1)
-BUCKET_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320, 322) for L in (8, 16, 32) for nr in (2049, 8192)
+BUCKET_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320, 322, 323) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (4095, 300007, (1 << 20) + 5)]
 
 
@@ -733,7 +733,7 @@ RECORD_CASES += [(8, nr, n, v) for v in (271, 272) for nr in (2049, 8192) for n 
 # 112: the r02 store order of 8-B records (header halves a staging round early)
 RECORD_CASES += [(8, nr, n, 112) for nr in (7, 1000, 1463) for n in (4097, (2 << 20) + 9)]
 # r06: records on the r02-r05 two-pass form (290) and the tile-local shapes 291-293
-RECORD_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320, 322) for L in (8, 16, 32) for nr in (2049, 8192)
+RECORD_CASES += [(L, nr, n, v) for v in (290, 291, 292, 293, 302, 304, 305, 316, 318, 320, 322, 323) for L in (8, 16, 32) for nr in (2049, 8192)
                  for n in (4097, 300007)]
 RECORD_CASES += [(L, 8192, (4 << 20) + 7, 0) for L in (8, 32)]
 
